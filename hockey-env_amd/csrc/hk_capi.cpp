@@ -1,0 +1,257 @@
+// hk_capi.cpp -- the extern "C" boundary declared in include/hockey.h.
+//
+// Owns the per-context device state (SoA arrays in HBM, allocated once at hk_create and sized for the
+// whole arena batch), validates arguments, and launches the gfx950 kernels on the caller's stream.
+// Errors are reported as negative status codes plus a thread-local message (hk_last_error); no C++
+// exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/hockey.h"
+#include "hk_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, const char *a = "", long long b = 0) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), fmt, a, b);
+  g_err = buf;
+  return code;
+}
+
+int hipfail(hipError_t e, const char *where) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(e));
+  g_err = buf;
+  return HK_E_HIP;
+}
+
+struct Ctx {
+  int device = 0;
+  hk::DevState s{};
+  hk::KCfg cfg{};
+  bool scene_ok = false;
+};
+
+bool g_scene_uploaded[64] = {false};
+
+int check_policy(int p) { return p >= HK_POLICY_EXTERNAL && p <= HK_POLICY_BASIC_STRONG; }
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char *hk_last_error(void) { return g_err.c_str(); }
+
+const char *hk_version(void) { return "hockey-mi355x 0.1 (gfx950, lane-per-arena step kernel)"; }
+
+int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
+  if (!out) return fail(HK_E_INVALID, "hk_create: out is NULL%s", "");
+  *out = nullptr;
+  if (n <= 0 || n > (int64_t)1 << 30) return fail(HK_E_INVALID, "hk_create: bad n_arenas %s%lld", "", n);
+  if (!cfg) return fail(HK_E_INVALID, "hk_create: cfg is NULL%s");
+  if (cfg->mode < 0 || cfg->mode > 2) return fail(HK_E_INVALID, "hk_create: bad mode%s");
+  if (!check_policy(cfg->policy[0]) || !check_policy(cfg->policy[1]))
+    return fail(HK_E_INVALID, "hk_create: bad policy%s");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) return fail(HK_E_DEVICE, "hk_create: no HIP device available%s");
+  if (device < 0 || device >= ndev) return fail(HK_E_DEVICE, "hk_create: device %s%lld out of range", "", device);
+  hipDeviceProp_t prop;
+  if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return hipfail(e, "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(HK_E_DEVICE, "hk_create: device arch %s is not gfx950 (MI355X)", prop.gcnArchName);
+  DeviceGuard g(device);
+  Ctx *c = new Ctx();
+  c->device = device;
+  c->cfg.keep_mode = cfg->keep_mode ? 1 : 0;
+  c->cfg.mode = cfg->mode;
+  c->cfg.auto_reset = cfg->auto_reset ? 1 : 0;
+  c->cfg.vel_ref = cfg->vel_ref_semantics ? 1 : 0;
+  c->cfg.policy[0] = cfg->policy[0];
+  c->cfg.policy[1] = cfg->policy[1];
+  c->cfg.seed = cfg->seed;
+  c->cfg.arena_offset = cfg->arena_offset;
+  c->s.n = n;
+  const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NIF * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
+  if ((e = hipMalloc(&c->s.f, nf * 4)) != hipSuccess || (e = hipMalloc(&c->s.i, ni * 4)) != hipSuccess ||
+      (e = hipMalloc(&c->s.man, nm * 4)) != hipSuccess || (e = hipMalloc(&c->s.phase, 2 * n * 8)) != hipSuccess ||
+      (e = hipMalloc(&c->s.counters, HK_NUM_COUNTERS * 8)) != hipSuccess) {
+    hk_destroy(c);
+    return hipfail(e, "hk_create: hipMalloc");
+  }
+  if (device < 64 && !g_scene_uploaded[device]) {
+    hk::Scene sc;
+    hk::build_scene(sc);
+    if ((e = hk::upload_scene(sc)) != hipSuccess) {
+      hk_destroy(c);
+      return hipfail(e, "hk_create: scene upload");
+    }
+    g_scene_uploaded[device] = true;
+  }
+  if ((e = hipMemset(c->s.counters, 0, HK_NUM_COUNTERS * 8)) != hipSuccess ||
+      (e = hipMemset(c->s.man, 0, nm * 4)) != hipSuccess) {
+    hk_destroy(c);
+    return hipfail(e, "hk_create: hipMemset");
+  }
+  if ((e = hk::launch_init(c->s, c->cfg, nullptr)) != hipSuccess) {
+    hk_destroy(c);
+    return hipfail(e, "hk_create: init kernel");
+  }
+  // HockeyEnv.__init__ ends with reset(one_starts=True) (hockey_env.py:155): device placement
+  if ((e = hk::launch_reset(c->s, c->cfg, nullptr, nullptr, nullptr, nullptr, nullptr)) != hipSuccess ||
+      (e = hipDeviceSynchronize()) != hipSuccess) {
+    hk_destroy(c);
+    return hipfail(e, "hk_create: initial reset");
+  }
+  *out = c;
+  return HK_OK;
+}
+
+int hk_destroy(void *ctx) {
+  if (!ctx) return HK_OK;
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  if (c->s.f) (void)hipFree(c->s.f);
+  if (c->s.i) (void)hipFree(c->s.i);
+  if (c->s.man) (void)hipFree(c->s.man);
+  if (c->s.phase) (void)hipFree(c->s.phase);
+  if (c->s.counters) (void)hipFree(c->s.counters);
+  delete c;
+  return HK_OK;
+}
+
+int64_t hk_num_arenas(const void *ctx) { return ctx ? ((const Ctx *)ctx)->s.n : 0; }
+
+int hk_set_policy(void *ctx, int player, int policy) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_set_policy: ctx is NULL%s");
+  if (player < 0 || player > 1 || !check_policy(policy)) return fail(HK_E_INVALID, "hk_set_policy: bad args%s");
+  ((Ctx *)ctx)->cfg.policy[player] = policy;
+  return HK_OK;
+}
+
+int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t *max_t, const uint8_t *one_starts,
+             void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_reset: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hk::launch_reset(c->s, c->cfg, mask, params, max_t, one_starts, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_reset");
+}
+
+int hk_step(void *ctx, const hk_step_io *io, void *stream) {
+  if (!ctx || !io) return fail(HK_E_INVALID, "hk_step: NULL argument%s");
+  Ctx *c = (Ctx *)ctx;
+  if (!io->actions && (c->cfg.policy[0] == HK_POLICY_EXTERNAL || c->cfg.policy[1] == HK_POLICY_EXTERNAL))
+    return fail(HK_E_INVALID, "hk_step: a player takes external actions but io->actions is NULL%s");
+  hk::StepIO s;
+  s.actions = io->actions;
+  s.opp_inc = io->opp_inc;
+  s.obs = io->obs;
+  s.obs2 = io->obs2;
+  s.reward = io->reward;
+  s.reward2 = io->reward2;
+  s.done = io->done;
+  s.info = io->info;
+  s.info2 = io->info2;
+  s.actions_out = io->actions_out;
+  s.debug = io->debug;
+  s.flags = io->flags;
+  DeviceGuard g(c->device);
+  hipError_t e = hk::launch_step(c->s, c->cfg, s, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_step");
+}
+
+int hk_get_state(void *ctx, float *state, int32_t *aux, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_get_state: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hk::launch_get_state(c->s, c->cfg, state, aux, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_get_state");
+}
+
+int hk_set_state(void *ctx, const uint8_t *mask, const float *state, const int32_t *aux, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_set_state: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hk::launch_set_state(c->s, c->cfg, mask, state, aux, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_set_state");
+}
+
+int hk_observe(void *ctx, float *obs, float *obs2, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_observe: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hk::launch_observe(c->s, c->cfg, obs, obs2, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_observe");
+}
+
+int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_opponent_phase: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hipSuccess;
+  const size_t bytes = (size_t)c->s.n * 2 * sizeof(double);
+  // device layout is [2][N] (player-major); the ABI layout is [N,2]
+  if (phase_out)
+    e = hipMemcpy2DAsync(phase_out, 2 * sizeof(double), c->s.phase, sizeof(double), sizeof(double), c->s.n,
+                         hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  if (e == hipSuccess && phase_out)
+    e = hipMemcpy2DAsync(phase_out + 1, 2 * sizeof(double), c->s.phase + c->s.n, sizeof(double), sizeof(double),
+                         c->s.n, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  if (e == hipSuccess && phase_in)
+    e = hipMemcpy2DAsync(c->s.phase, sizeof(double), phase_in, 2 * sizeof(double), sizeof(double), c->s.n,
+                         hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  if (e == hipSuccess && phase_in)
+    e = hipMemcpy2DAsync(c->s.phase + c->s.n, sizeof(double), phase_in + 1, 2 * sizeof(double), sizeof(double),
+                         c->s.n, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  (void)bytes;
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_opponent_phase");
+}
+
+int hk_counters(void *ctx, int64_t *out, void *stream) {
+  if (!ctx || !out) return fail(HK_E_INVALID, "hk_counters: NULL argument%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hipMemcpyAsync(out, c->s.counters, HK_NUM_COUNTERS * 8, hipMemcpyDeviceToHost, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_counters");
+}
+
+int hk_reset_counters(void *ctx, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_reset_counters: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hipMemsetAsync(c->s.counters, 0, HK_NUM_COUNTERS * 8, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_reset_counters");
+}
+
+int hk_bytes_per_step(const void *ctx, int64_t *algorithmic, int64_t *implementation) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_bytes_per_step: ctx is NULL%s");
+  // action 32 B + body state 72 B + 4 int32 scalars 16 B read; body state 72 B,
+  // scalars 16 B, obs 72 B, reward 4 B, done 1 B written = 285 B per env-step.
+  if (algorithmic) *algorithmic = 285;
+  // implementation (excluding manifolds, which are only touched where a pair is in contact):
+  // f: 29 floats read+write, i: 12 ints read+write, obs 72 + reward 4 + done 1 + info 16.
+  if (implementation) *implementation = (int64_t)(hk::NFF * 4 * 2 + hk::NIF * 4 * 2 + 72 + 4 + 1 + 16);
+  return HK_OK;
+}
+
+}  // extern "C"

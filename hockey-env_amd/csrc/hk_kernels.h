@@ -1,0 +1,58 @@
+// hk_kernels.h -- host/device shared declarations: HBM state layout and kernel launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hk_core.h"
+
+namespace hk {
+
+// per dynamic body float fields (f[b*FB + k][N])
+enum { FB_PX = 0, FB_PY, FB_CX, FB_CY, FB_A, FB_VX, FB_VY, FB_W, FB_SLEEP, FB };
+enum { F_PFX = 3 * FB, F_PFY, NFF };
+// int fields
+enum { I_AWAKE = 0, I_HAS1, I_HAS2, I_TIME, I_DONE, I_WINNER, I_MAXT, I_TOUCH, I_ENABLED, I_ONE, I_EPISODE, I_STEP, NIF };
+// manifold fields per solid pair
+enum { M_META = 0, M_LNX, M_LNY, M_LPX, M_LPY, M_P0X, M_P0Y, M_P0ID, M_P0NI, M_P0TI, M_P1X, M_P1Y, M_P1ID, M_P1NI,
+       M_P1TI, NMF };
+
+struct DevState {
+  float *f;
+  int32_t *i;
+  float *man;
+  double *phase;
+  unsigned long long *counters;
+  int64_t n;
+};
+
+struct KCfg {
+  int keep_mode, mode, auto_reset, vel_ref;
+  int policy[2];
+  uint64_t seed;
+  int64_t arena_offset;
+};
+
+struct StepIO {
+  const float *actions;
+  const double *opp_inc;
+  float *obs, *obs2, *reward, *reward2;
+  uint8_t *done;
+  float *info, *info2, *actions_out, *debug;
+  int flags;
+};
+
+hipError_t launch_init(const DevState &s, const KCfg &cfg, hipStream_t st);
+hipError_t launch_reset(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *params,
+                        const int32_t *max_t, const uint8_t *one, hipStream_t st);
+hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, hipStream_t st);
+hipError_t launch_observe(const DevState &s, const KCfg &cfg, float *obs, float *obs2, hipStream_t st);
+hipError_t launch_get_state(const DevState &s, const KCfg &cfg, float *state, int32_t *aux, hipStream_t st);
+hipError_t launch_set_state(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *state,
+                            const int32_t *aux, hipStream_t st);
+hipError_t upload_scene(const Scene &sc);
+
+// host-side scene construction (hk_scene.cpp): Box2D 2.3 hull / normals / mass data of hockey_env.py's
+// fixtures, and the canonical contact pair table.
+void build_scene(Scene &sc);
+
+}  // namespace hk

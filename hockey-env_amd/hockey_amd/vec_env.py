@@ -1,0 +1,225 @@
+"""VecHockeyEnv: N independent arenas resident in HBM, stepped by the gfx950 kernel.
+
+This is the batched form of ``HockeyEnv`` (hockey/hockey_env.py:83-779): every call maps one-to-one
+onto the reference's per-env call, vectorised over a leading arena axis and kept on the device:
+
+  ========================================  ================================================
+  reference (one env, numpy, host)          VecHockeyEnv (N arenas, torch tensors on cuda)
+  ========================================  ================================================
+  reset(seed=s)            :345              reset(seeds=[...]) / reset() (device placement)
+  step(a[8]) -> obs,r,d,_,info :658          step(actions[N,8]) -> obs[N,18], r[N], d[N], info
+  obs_agent_two()          :500              obs_agent_two()  (or step(..., with_agent_two=True))
+  get_info_agent_two()/get_reward_agent_two  returned by step(..., with_agent_two=True)
+  set_state(s[18])         :594              set_state(state[N,18] raw, aux[N,5])
+  BasicOpponent.act        :787              policy=('external'|'random'|'weak'|'strong') per player
+  ========================================  ================================================
+
+Torch is plumbing only (device memory + the current HIP stream); the compute is libhockey_hip.so.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .constants import Mode, parse_mode
+from .placement import np_random, placement
+
+_POLICIES = {"external": N.POLICY_EXTERNAL, "random": N.POLICY_RANDOM, "weak": N.POLICY_BASIC_WEAK,
+             "strong": N.POLICY_BASIC_STRONG}
+
+
+def _policy_id(p):
+    if isinstance(p, int):
+        return p
+    return _POLICIES[p]
+
+
+class StepResult:
+    __slots__ = ("obs", "reward", "done", "info", "obs2", "reward2", "info2", "actions")
+
+    def __init__(self, **kw):
+        for k in self.__slots__:
+            setattr(self, k, kw.get(k))
+
+
+class VecHockeyEnv:
+    """Batched hockey arenas on one MI355X (one context per device and stream)."""
+
+    def __init__(self, n_arenas, keep_mode=True, mode=Mode.NORMAL, device=None, policies=("external", "external"),
+                 auto_reset=False, seed=0, vel_ref_semantics=False, arena_offset=0):
+        if not torch.cuda.is_available():
+            raise N.HockeyNativeError("VecHockeyEnv needs a ROCm GPU (gfx950); the hot path has no CPU fallback")
+        self.L = N.lib()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.n = int(n_arenas)
+        self.keep_mode = bool(keep_mode)
+        self.mode = parse_mode(mode)
+        self.auto_reset = bool(auto_reset)
+        cfg = N.Config()
+        cfg.keep_mode = int(self.keep_mode)
+        cfg.mode = self.mode.value
+        cfg.auto_reset = int(self.auto_reset)
+        cfg.vel_ref_semantics = int(bool(vel_ref_semantics))
+        cfg.policy[0] = _policy_id(policies[0])
+        cfg.policy[1] = _policy_id(policies[1])
+        cfg.seed = int(seed) & ((1 << 64) - 1)
+        cfg.arena_offset = int(arena_offset)
+        self.arena_offset = int(arena_offset)
+        self.policies = [cfg.policy[0], cfg.policy[1]]
+        ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            N.check(self.L.hk_create(self.device.index, self.n, ctypes.byref(cfg), ctypes.byref(ctx)), "hk_create")
+        self._ctx = ctx
+        self.one_starts = np.ones(self.n, bool)  # HockeyEnv.__init__ resets with one_starting=True
+        self._alloc()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        d, n = self.device, self.n
+        self.obs_buf = torch.zeros((n, N.OBS_DIM), dtype=torch.float32, device=d)
+        self.obs2_buf = torch.zeros((n, N.OBS_DIM), dtype=torch.float32, device=d)
+        self.reward_buf = torch.zeros((n,), dtype=torch.float32, device=d)
+        self.reward2_buf = torch.zeros((n,), dtype=torch.float32, device=d)
+        self.done_buf = torch.zeros((n,), dtype=torch.uint8, device=d)
+        self.info_buf = torch.zeros((n, N.INFO_DIM), dtype=torch.float32, device=d)
+        self.info2_buf = torch.zeros((n, N.INFO_DIM), dtype=torch.float32, device=d)
+        self.actions_buf = torch.zeros((n, N.ACT_DIM), dtype=torch.float32, device=d)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self.L.hk_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def set_policy(self, player, policy):
+        pid = _policy_id(policy)
+        N.check(self.L.hk_set_policy(self._ctx, int(player), pid), "hk_set_policy")
+        self.policies[player] = pid
+
+    # ------------------------------------------------------------------ reset
+    def reset(self, seeds=None, mask=None, one_starting=None):
+        """HockeyEnv.reset for the selected arenas.
+
+        seeds: None -> device Philox placement; int / sequence -> the reference's PCG64 draws per arena
+        (bit-identical placement to ``HockeyEnv.reset(seed=s)``).  one_starting: None toggles like the
+        reference (NORMAL mode), a bool / bool array forces the puck side.
+        Returns (obs[N,18], info[N,4]) tensors (agent-1 frame) for all arenas.
+        """
+        n = self.n
+        sel = np.ones(n, bool) if mask is None else np.asarray(mask.cpu() if torch.is_tensor(mask) else mask, bool)
+        if self.mode == Mode.NORMAL:
+            if one_starting is None:
+                self.one_starts = np.where(sel, ~self.one_starts, self.one_starts)
+            else:
+                self.one_starts = np.where(sel, np.broadcast_to(np.asarray(one_starting, bool), (n,)), self.one_starts)
+        one_t = torch.as_tensor(self.one_starts.astype(np.uint8), device=self.device)
+        mask_t = None if mask is None else torch.as_tensor(sel.astype(np.uint8), device=self.device)
+        params_t = None
+        if seeds is not None:
+            seeds = np.broadcast_to(np.asarray(seeds, dtype=object), (n,))
+            params = np.zeros((n, N.PARAM_DIM), np.float32)
+            for i in np.nonzero(sel)[0]:
+                rng, _ = np_random(None if seeds[i] is None else int(seeds[i]))
+                params[i], _ = placement(self.mode, bool(self.one_starts[i]), rng)
+            params_t = torch.as_tensor(params, device=self.device)
+        N.check(self.L.hk_reset(self._ctx, N.ptr(mask_t), N.ptr(params_t), None, N.ptr(one_t), self._stream()),
+                "hk_reset")
+        return self.observe()
+
+    def reset_params(self, params, mask=None, max_t=None):
+        """Reset from explicit placement vectors [N,6] (float32 on device)."""
+        mask_t = None if mask is None else torch.as_tensor(mask, dtype=torch.uint8, device=self.device)
+        mt = None if max_t is None else torch.as_tensor(max_t, dtype=torch.int32, device=self.device)
+        params = torch.as_tensor(params, dtype=torch.float32, device=self.device).contiguous()
+        N.check(self.L.hk_reset(self._ctx, N.ptr(mask_t), N.ptr(params), N.ptr(mt), None, self._stream()), "hk_reset")
+
+    # ------------------------------------------------------------------ step
+    def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=None, skip_physics=False,
+             record_actions=False):
+        """HockeyEnv.step for every arena.  actions: [N,8] float (clipped in-kernel), may be None when no
+        player is external.  Returns a StepResult of device tensors (views of persistent buffers)."""
+        a = None
+        if actions is not None:
+            a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
+            if a.shape != (self.n, N.ACT_DIM):
+                raise ValueError(f"actions must have shape ({self.n}, {N.ACT_DIM}), got {tuple(a.shape)}")
+            a = a.contiguous()
+        inc = None
+        if opp_inc is not None:
+            inc = torch.as_tensor(opp_inc, dtype=torch.float64, device=self.device).contiguous()
+        io = N.StepIO()
+        io.actions = None if a is None else a.data_ptr()
+        io.opp_inc = None if inc is None else inc.data_ptr()
+        io.obs = self.obs_buf.data_ptr()
+        io.reward = self.reward_buf.data_ptr()
+        io.done = self.done_buf.data_ptr()
+        io.info = self.info_buf.data_ptr()
+        if with_agent_two:
+            io.obs2 = self.obs2_buf.data_ptr()
+            io.reward2 = self.reward2_buf.data_ptr()
+            io.info2 = self.info2_buf.data_ptr()
+        if record_actions:
+            io.actions_out = self.actions_buf.data_ptr()
+        if debug is not None:
+            io.debug = debug.data_ptr()
+        io.flags = N.STEP_SKIP_PHYSICS if skip_physics else 0
+        N.check(self.L.hk_step(self._ctx, ctypes.byref(io), self._stream()), "hk_step")
+        return StepResult(obs=self.obs_buf, reward=self.reward_buf, done=self.done_buf, info=self.info_buf,
+                          obs2=self.obs2_buf if with_agent_two else None,
+                          reward2=self.reward2_buf if with_agent_two else None,
+                          info2=self.info2_buf if with_agent_two else None,
+                          actions=self.actions_buf if record_actions else None)
+
+    def step_raw(self, io):
+        """Launch one step with a prepared StepIO (no Python-side allocation; for benchmarks)."""
+        N.check(self.L.hk_step(self._ctx, ctypes.byref(io), self._stream()), "hk_step")
+
+    # ------------------------------------------------------------------ state / obs
+    def observe(self):
+        N.check(self.L.hk_observe(self._ctx, N.ptr(self.obs_buf), N.ptr(self.obs2_buf), self._stream()), "hk_observe")
+        return self.obs_buf, self.obs2_buf
+
+    def obs_agent_two(self):
+        return self.observe()[1]
+
+    def get_state(self):
+        st = torch.zeros((self.n, N.STATE_DIM), dtype=torch.float32, device=self.device)
+        aux = torch.zeros((self.n, N.AUX_DIM), dtype=torch.int32, device=self.device)
+        N.check(self.L.hk_get_state(self._ctx, N.ptr(st), N.ptr(aux), self._stream()), "hk_get_state")
+        return st, aux
+
+    def set_state(self, state=None, aux=None, mask=None):
+        st = None if state is None else torch.as_tensor(state, dtype=torch.float32, device=self.device).contiguous()
+        ax = None if aux is None else torch.as_tensor(aux, dtype=torch.int32, device=self.device).contiguous()
+        mk = None if mask is None else torch.as_tensor(mask, dtype=torch.uint8, device=self.device).contiguous()
+        N.check(self.L.hk_set_state(self._ctx, N.ptr(mk), N.ptr(st), N.ptr(ax), self._stream()), "hk_set_state")
+
+    def opponent_phase(self, new_phase=None):
+        """Return the BasicOpponent phases [N,2] (float64, device); optionally overwrite them."""
+        out = torch.zeros((self.n, 2), dtype=torch.float64, device=self.device)
+        ph = None if new_phase is None else torch.as_tensor(new_phase, dtype=torch.float64,
+                                                            device=self.device).contiguous()
+        N.check(self.L.hk_opponent_phase(self._ctx, N.ptr(out), N.ptr(ph), self._stream()), "hk_opponent_phase")
+        return out
+
+    def counters(self):
+        out = (ctypes.c_int64 * N.NUM_COUNTERS)()
+        N.check(self.L.hk_counters(self._ctx, out, self._stream()), "hk_counters")
+        return np.array(out[:], np.int64)
+
+    def reset_counters(self):
+        N.check(self.L.hk_reset_counters(self._ctx, self._stream()), "hk_reset_counters")
+
+    def bytes_per_step(self):
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        N.check(self.L.hk_bytes_per_step(self._ctx, ctypes.byref(a), ctypes.byref(b)), "hk_bytes_per_step")
+        return a.value, b.value

@@ -49,7 +49,7 @@ def lib():
                                          ctypes.c_double, _f64p, _f64p]
         L.hko_stats.argtypes = [ctypes.c_void_p, _i32p]
         L.hko_bench_random.restype = ctypes.c_int64
-        L.hko_bench_random.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+        L.hko_bench_random.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
@@ -129,7 +129,8 @@ def geometry():
     return out[:n]
 
 
-def bench_random(n_arenas, steps, threads=0, seed=0):
+def bench_random(n_arenas, steps, threads=0, seed=0, policy="random"):
     sec = ctypes.c_double()
-    total = lib().hko_bench_random(int(n_arenas), int(steps), int(threads), int(seed), ctypes.byref(sec))
+    pol = {"random": 0, "basic": 1}[policy]
+    total = lib().hko_bench_random(int(n_arenas), int(steps), int(threads), int(seed), pol, ctypes.byref(sec))
     return int(total), sec.value

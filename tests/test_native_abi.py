@@ -1,0 +1,63 @@
+"""The C-ABI library loads and exports every symbol include/hockey.h declares (no GPU needed, no
+compute calls), and the ctypes structures match the header's layout."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "hockey.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hk_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_boundary():
+    names = _declared()
+    for required in ("hk_create", "hk_destroy", "hk_reset", "hk_step", "hk_get_state", "hk_set_state",
+                     "hk_observe", "hk_last_error"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from hockey_amd import _native as N
+
+    if not os.path.exists(N.LIB_PATH):
+        N.build()
+    L = ctypes.CDLL(N.LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(_declared()) == set(N.EXPORTS)
+    lib = N.lib()
+    assert b"gfx950" in lib.hk_version()
+
+
+def test_ctypes_struct_layout_matches_header():
+    from hockey_amd import _native as N
+
+    # hk_config: 4 x int32, int32[2], uint64, int64 -> 40 bytes; hk_step_io: 11 pointers + int32 (padded)
+    assert ctypes.sizeof(N.Config) == 40
+    assert N.Config.seed.offset == 24 and N.Config.arena_offset.offset == 32
+    assert ctypes.sizeof(N.StepIO) == 96 and N.StepIO.flags.offset == 88
+
+
+def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
+    """Missing native library -> loud failure, never a silent Python/oracle path."""
+    from hockey_amd import _native as N
+
+    monkeypatch.setattr(N, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(N, "_lib", None)
+    with pytest.raises(N.HockeyNativeError):
+        N.lib()
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "hockey-env_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                text = open(os.path.join(dirpath, f), errors="replace").read()
+                assert "hk_oracle" not in text and "import oracle" not in text, f

@@ -1,0 +1,134 @@
+"""Pin the CPU oracle against the golden vectors generated from the reference module itself.
+
+Golden provenance: tests/golden/make_golden.py imports /root/reference/hockey/hockey_env.py with stub
+Box2D/gymnasium modules and a pybox2d-semantics fake world (world.Step is a no-op there), so these
+vectors pin everything around the Box2D solve bit-exactly: reset placement (G1), the pre-solve force /
+torque / damping laws, hold + shoot, obs / obs_agent_two / info / reward / done (G2),
+BasicOpponent.act (G4), and the discrete map / mode parsing (G5).  G6 (mass data) is our float32
+restatement of Box2D's polygon code, cross-checked against the oracle's independent computation.
+"""
+import numpy as np
+import pytest
+
+from hockey_amd.placement import np_random, placement
+
+
+def test_g6_geometry_matches_oracle(oracle, golden):
+    g6 = golden("g6_geometry.npz")
+    ref = np.concatenate([g6["player1_verts"].ravel(), g6["player1_normals"].ravel(), g6["player1_mass"],
+                          g6["player2_verts"].ravel(), g6["player2_normals"].ravel(), g6["player2_mass"],
+                          g6["puck_mass"]])
+    geo = oracle.geometry()
+    assert geo.shape == ref.shape
+    assert np.array_equal(geo, ref)
+    # mirrored racket is NOT the same float32 mass (58.000004 vs 58.0): both must be kept per player
+    assert g6["player1_mass"][0] != g6["player2_mass"][0]
+
+
+def test_g1_reset_placement_and_obs(oracle, golden):
+    g1 = golden("g1_reset.npz")
+    worlds = {m: oracle.OracleWorld(True, m) for m in (0, 1, 2)}
+    for i in range(len(g1["seed"])):
+        mode, seed, one = int(g1["mode"][i]), int(g1["seed"][i]), bool(g1["one_starts"][i])
+        rng, _ = np_random(seed)
+        params, max_t = placement(mode, one, rng)
+        st = g1["state"][i]
+        exp = np.array([st[6], st[7], st[12], st[13], *g1["puck_force"][i]], np.float32)
+        assert np.array_equal(params, exp), (i, params, exp)
+        assert max_t == g1["max_t"][i]
+        w = worlds[mode]
+        w.reset(params, max_t)
+        assert np.array_equal(w.obs().astype(np.float64), g1["obs"][i]), i
+
+
+G2_FIELDS = ["force", "torque", "ldamp", "adamp", "state_after", "has_after", "obs", "obs2", "reward", "reward2",
+             "done", "info", "info2"]
+
+
+def _run_g2_case(oracle, g2, i, worlds):
+    keep, mode = bool(g2["keep_mode"][i]), int(g2["mode"][i])
+    w = worlds[(keep, mode)]
+    w.reset(np.array([8, 4, 3, 4, 0, 0], np.float32), 250 if mode == 0 else 80)
+    w.set_raw(g2["state"][i], g2["aux"][i])
+    obs, r, d, info, dbg = w.step(g2["action"][i], skip_physics=True)
+    st, aux = w.get_raw()
+    i2, r2 = w.info_two()
+    return {"force": dbg[0:6].reshape(3, 2), "torque": dbg[6:8], "ldamp": dbg[8:11], "adamp": dbg[11:13],
+            "state_after": st, "has_after": aux[[0, 1, 2]], "obs": obs.astype(np.float64),
+            "obs2": w.obs_two().astype(np.float64), "reward": r, "reward2": r2, "done": int(d), "info": info,
+            "info2": i2}
+
+
+def test_g2_step_laws_bit_exact(oracle, golden):
+    g2 = golden("g2_step_presolve.npz")
+    worlds = {(k, m): oracle.OracleWorld(k, m) for k in (True, False) for m in (0, 1, 2)}
+    bad = {}
+    for i in range(len(g2["mode"])):
+        got = _run_g2_case(oracle, g2, i, worlds)
+        for f in G2_FIELDS:
+            if not np.array_equal(np.asarray(got[f]), g2[f][i]):
+                bad.setdefault(f, []).append(i)
+    assert not bad, {k: v[:5] for k, v in bad.items()}
+
+
+def test_g2_covers_every_branch(golden):
+    """The fixture exercises centre-zone, max-speed, boundary, angle-limit, hold and shoot branches."""
+    g2 = golden("g2_step_presolve.npz")
+    st, aux = g2["state"], g2["aux"]
+    assert (st[:, 0] > 4.5).sum() > 100 and (st[:, 6] < 5.5).sum() > 100        # centre zone
+    assert (np.hypot(st[:, 3], st[:, 4]) >= 10).sum() > 100                        # over max speed
+    assert (np.abs(st[:, 2]) > np.pi / 3).sum() > 100                               # angle limit
+    assert ((st[:, 1] > 6.8) | (st[:, 1] < 1.2)).sum() > 100                        # y boundary
+    assert (aux[:, 0] > 1).sum() > 100 and (g2["force"][:, 2] != 0).any(axis=1).sum() > 100  # hold + shoot
+    assert (g2["nforce"][:, 0] == 0).sum() + (g2["nforce"][:, 1] == 0).sum() > 10    # no-force branch
+    assert (g2["done"] == 1).sum() > 100 and (g2["keep_mode"] == 0).sum() > 100
+
+
+def test_g4_basic_opponent(oracle, golden):
+    """BasicOpponent.act: bit-exact after the env's float32 cast (hockey_env.py:659); <=1 ulp in double
+    (deterministic fdlibm sin vs the platform libm)."""
+    g4 = golden("g4_basic_opponent.npz")
+    for i in range(len(g4["act"])):
+        a, ph = oracle.basic_opponent(g4["weak"][i], g4["keep"][i], g4["phase0"][i], g4["inc"][i], g4["obs"][i])
+        assert ph == g4["phase"][i]
+        assert np.array_equal(a.astype(np.float32), g4["act"][i].astype(np.float32)), i
+        np.testing.assert_allclose(a, g4["act"][i], rtol=0, atol=1e-15)
+
+
+def test_g5_discrete_and_modes(golden):
+    from hockey_amd.constants import parse_mode
+
+    g5 = golden("g5_discrete_modes.npz")
+    from hockey_amd.hockey_env import HockeyEnv
+
+    disc = np.array([HockeyEnv.discrete_to_continous_action(type("E", (), {"keep_mode": True})(), i)
+                     for i in range(8)])
+    discn = np.array([HockeyEnv.discrete_to_continous_action(type("E", (), {"keep_mode": False})(), i)
+                      for i in range(8)])
+    assert np.array_equal(disc, g5["disc"]) and np.array_equal(discn, g5["disc_nokeep"])
+    for raw, kind, val in zip(g5["mode_in"], g5["mode_kind"], g5["mode_val"]):
+        v, t = str(raw).rsplit(":", 1)
+        x = {"str": str, "int": int, "float": float}[t](v)
+        try:
+            m = parse_mode(x)
+            assert kind == "ok" and m.value == int(val)
+        except ValueError:
+            assert kind == "ValueError"
+        except TypeError:
+            assert kind == "TypeError"
+    assert str(g5["reset_mode"]) == "TypeError"
+    assert int(g5["discrete_n"]) == 7 and tuple(g5["obs_shape"]) == (18,) and tuple(g5["act_shape"]) == (8,)
+
+
+@pytest.mark.parametrize("keep", [True, False])
+def test_oracle_mirror_symmetry(oracle, keep):
+    """obs_agent_two mirrors positions/velocities and swaps has_puck (hockey_env.py:500-516)."""
+    w = oracle.OracleWorld(keep, 0)
+    rng = np.random.default_rng(3)
+    w.reset(np.array([8, 4, 6.5, 3.7, 0, 0], np.float32), 250)
+    for _ in range(50):
+        w.step(rng.uniform(-1, 1, 8).astype(np.float32))
+        o, o2 = w.obs(), w.obs_two()
+        assert np.array_equal(o2[0:2], -o[6:8]) and np.array_equal(o2[6:8], -o[0:2])
+        assert np.array_equal(o2[3:5], -o[9:11]) and np.array_equal(o2[12:16], -o[12:16])
+        assert o2[2] == o[8] and o2[8] == o[2] and o2[16] == o[17] and o2[17] == o[16]
