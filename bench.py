@@ -29,8 +29,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--arenas", type=int, default=65536, help="arenas per GPU")
     ap.add_argument("--policy", choices=["basic", "random"], default="basic")
     ap.add_argument("--seed", type=int, default=0)

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -89,6 +90,8 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   c->cfg.policy[1] = cfg->policy[1];
   c->cfg.seed = cfg->seed;
   c->cfg.arena_offset = cfg->arena_offset;
+  c->cfg.ablate = 0;
+  if (const char *ab = std::getenv("HK_ABLATE")) c->cfg.ablate = std::atoi(ab);  // timing experiments only
   c->s.n = n;
   const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NIF * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
   if ((e = hipMalloc(&c->s.f, nf * 4)) != hipSuccess || (e = hipMalloc(&c->s.i, ni * 4)) != hipSuccess ||

@@ -62,7 +62,13 @@ struct Scene {
   float friction[NP], restitution[NP];
   int manslot[NP];                                             // manifold slot or -1 (sensor)
   int edges[3][10];                                            // contact edges of each dynamic body
+  // broad-phase rejection data (performance only; results unchanged, see hk_world.h pair_far_*)
+  float fx_aabb[NF][4];   // world AABB of every static fixture {minx, miny, maxx, maxy}
+  float rcore[3];         // max distance from a dynamic body's COM to its core (radius-free) shape
 };
+
+// margin of the conservative rejection tests: covers float rounding of transforms / sweep interpolation
+constexpr float kFarMargin = 0.05f;
 
 // ---------------------------------------------------------------------------------------------
 // float32 algebra (b2Math.h)
@@ -204,5 +210,21 @@ HK_DEV double hk_cos(double x) {
     default: return ksin(a, b);
   }
 }
+
+// Diagnostic build only (make TIMERS=1): per-phase shader-clock accounting; compiled out otherwise.
+#ifdef HK_PHASE_TIMERS
+struct PhaseT {
+  unsigned long long last, acc[8];
+};
+#define HK_TIC(T, k)                                              \
+  do {                                                            \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();         \
+    (T).acc[k] += _t - (T).last;                                  \
+    (T).last = _t;                                                \
+  } while (0)
+#else
+struct PhaseT {};
+#define HK_TIC(T, k) ((void)0)
+#endif
 
 }  // namespace hk

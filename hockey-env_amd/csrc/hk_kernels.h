@@ -30,6 +30,7 @@ struct KCfg {
   int policy[2];
   uint64_t seed;
   int64_t arena_offset;
+  int ablate;  // timing-only ablations (bit0 vel iters, bit1 pos iters, bit2 TOI, bit3 collide); 0 in product
 };
 
 struct StepIO {

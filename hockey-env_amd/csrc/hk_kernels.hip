@@ -13,7 +13,7 @@
 
 __constant__ hk::Scene g_scene;
 
-#include "hk_world.h"
+#include "hk_fast.h"
 #include "hk_kernels.h"
 
 namespace hk {
@@ -281,6 +281,11 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = a < s.n;
   int done_edge = 0, win1 = 0, win2 = 0, ntoi = 0, ovf = 0;
+  PhaseT T;
+#ifdef HK_PHASE_TIMERS
+  for (int k = 0; k < 8; ++k) T.acc[k] = 0;
+  T.last = __builtin_amdgcn_s_memtime();
+#endif
   if (live) {
     World w;
     Solver S;
@@ -329,7 +334,9 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
       for (int k = 0; k < 8; ++k) io.actions_out[a * 8 + k] = a8[k];
     // ---- HockeyEnv.step ----
     const int was_done = w.done;
+    HK_TIC(T, 0);
     presolve(w, a8);
+    HK_TIC(T, 1);
     if (io.debug) {
       float *d = io.debug + a * 13;
       d[0] = w.b[B_P1].force.x; d[1] = w.b[B_P1].force.y; d[2] = w.b[B_P2].force.x; d[3] = w.b[B_P2].force.y;
@@ -337,7 +344,7 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
       d[8] = w.b[B_P1].ld; d[9] = w.b[B_P2].ld; d[10] = w.b[B_PK].ld; d[11] = w.b[B_P1].ad; d[12] = w.b[B_P2].ad;
     }
     if (!(io.flags & 1)) {
-      world_step(w, S);
+      world_step(w, S, cfg.ablate, T);
     } else {
       for (int i = 0; i < 3; ++i) { w.b[i].force = V(0.0f, 0.0f); w.b[i].torque = 0.0f; }
     }
@@ -365,6 +372,7 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
     w.time += 1;
     store_world(w, s, a);
     I(s, I_STEP, a) = (int)(stepc + 1);
+    HK_TIC(T, 5);
     done_edge = (!was_done && w.done);
     win1 = done_edge && w.winner == 1;
     win2 = done_edge && w.winner == -1;
@@ -380,6 +388,10 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
     if (ntoi > 0) atomicAdd(&s.counters[4], (unsigned long long)ntoi);
   }
   wave_count(s.counters, 5, ovf);
+#ifdef HK_PHASE_TIMERS
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&s.counters[8 + k], T.acc[k]);
+#endif
 }
 
 __global__ void __launch_bounds__(64) observe_kernel(DevState s, KCfg cfg, float *obs, float *obs2) {

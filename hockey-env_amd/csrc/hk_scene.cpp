@@ -212,6 +212,26 @@ void build_scene(Scene &sc) {
     sc.restitution[p] = fA.restitution > fB.restitution ? fA.restitution : fB.restitution;  // b2MixRestitution
     sc.manslot[p] = sc.sensor[p] ? -1 : slot++;
   }
+  for (int f = 0; f < NF; ++f) {
+    const Fixture &fx = sc.fx[f];
+    if (fx.body < B_WT) continue;
+    float mnx = 1e30f, mny = 1e30f, mxx = -1e30f, mxy = -1e30f;
+    for (int k = 0; k < fx.count; ++k) {
+      float x = fx.vx[k] + sc.spx[fx.body], y = fx.vy[k] + sc.spy[fx.body];
+      mnx = x < mnx ? x : mnx; mny = y < mny ? y : mny; mxx = x > mxx ? x : mxx; mxy = y > mxy ? y : mxy;
+    }
+    sc.fx_aabb[f][0] = mnx; sc.fx_aabb[f][1] = mny; sc.fx_aabb[f][2] = mxx; sc.fx_aabb[f][3] = mxy;
+  }
+  for (int b = 0; b < 3; ++b) {
+    const Fixture &fx = sc.fx[b == B_PK ? F_PK : (b == B_P1 ? F_P1 : F_P2)];
+    float r = 0.0f;
+    for (int k = 0; k < fx.count; ++k) {
+      float dx = fx.vx[k] - sc.lcx[b], dy = fx.vy[k] - sc.lcy[b];
+      float d = std::sqrt(dx * dx + dy * dy);
+      r = d > r ? d : r;
+    }
+    sc.rcore[b] = r;
+  }
   const int e1[10] = {8, 10, 11, 12, 13, 14, 15, 16, 17, 18};
   const int e2[10] = {9, 10, 19, 20, 21, 22, 23, 24, 25, 26};
   for (int k = 0; k < 10; ++k) {

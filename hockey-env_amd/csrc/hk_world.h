@@ -654,6 +654,62 @@ HK_DEV void contact_update(World &w, int p) {
   if (!was && touching) begin_contact(w, p);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Lane-local broad phase.  Box2D only evaluates a pair once its fat AABBs overlap; here every pair
+// of the fixed table is live, so a conservative bounding test decides when the exact narrow phase /
+// time of impact cannot produce a contact point, a sensor overlap or a TOI "touching" event.  In that
+// case the pair takes exactly the outcome the full computation would have produced (touching = 0,
+// manifold count 0, alpha = 1), so results are bit-identical to the exhaustive oracle
+// (tests/test_gpu_parity.py runs the oracle WITHOUT this filter).
+//   * Box2D polygon clipping can emit points up to sqrt(2) * totalRadius from the reference polygon
+//     and the circle manifold up to totalRadius: reach = 2 * (rA + rB).
+//   * every TOI "touching" exit needs the core distance below target + tol < rA + rB at some t
+//     (GJK distance, or an axis separation that upper-bounds it, b2TimeOfImpact).
+// ------------------------------------------------------------------------------------------------
+HK_DEV float box_gap(float ax0, float ay0, float ax1, float ay1, const float *b) {
+  return fmaxf(fmaxf(b[0] - ax1, ax0 - b[2]), fmaxf(b[1] - ay1, ay0 - b[3]));
+}
+
+HK_DEV bool pair_far_collide(const World &w, int p) {
+  const int fA = SC.pairA[p], fB = SC.pairB[p];
+  const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
+  const Body &B = w.b[bB];
+  const float rB = SC.rcore[bB];
+  if (bA >= B_WT) {
+    return box_gap(B.c.x - rB, B.c.y - rB, B.c.x + rB, B.c.y + rB, SC.fx_aabb[fA]) > reach;
+  }
+  const Body &A = w.b[bA];
+  const float lim = SC.rcore[bA] + rB + reach;
+  const float dx = A.c.x - B.c.x, dy = A.c.y - B.c.y;
+  return dx * dx + dy * dy > lim * lim;
+}
+
+HK_DEV bool pair_far_toi(const World &w, int p) {  // static A, dynamic B, sweeps already aligned
+  const int fA = SC.pairA[p], fB = SC.pairB[p];
+  const Body &B = w.b[SC.pbodyB[p]];
+  const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
+  const float r = SC.rcore[SC.pbodyB[p]];
+  return box_gap(fminf(B.c0.x, B.c.x) - r, fminf(B.c0.y, B.c.y) - r, fmaxf(B.c0.x, B.c.x) + r,
+                 fmaxf(B.c0.y, B.c.y) + r, SC.fx_aabb[fA]) > reach;
+}
+
+// contact_update for a pair the broad phase rejected: the exact result of contact_update with no
+// manifold point / no overlap
+HK_DEV void contact_update_far(World &w, int p) {
+  Contact &c = w.c[p];
+  c.enabled = 1;
+  const int was = c.touching;
+  c.m.count = 0;
+  if (!SC.sensor[p] && was) { set_awake(w.b[SC.pbodyA[p]], 1); set_awake(w.b[SC.pbodyB[p]], 1); }
+  c.touching = 0;
+}
+
+HK_DEV void contact_update_any(World &w, int p) {
+  if (pair_far_collide(w, p)) contact_update_far(w, p);
+  else contact_update(w, p);
+}
+
 HK_DEV void collide(World &w) {
   for (int p = 0; p < NP; ++p) {
     Body &bA = w.b[SC.pbodyA[p]];
@@ -661,7 +717,7 @@ HK_DEV void collide(World &w) {
     int activeA = bA.awake && bA.dynamic;
     int activeB = bB.awake && bB.dynamic;
     if (!activeA && !activeB) continue;
-    contact_update(w, p);
+    contact_update_any(w, p);
   }
 }
 
@@ -997,7 +1053,7 @@ HK_DEV void integrate_positions(float h, PosV *P, VelV *Vl, int n) {
   }
 }
 
-HK_DEV void solve_islands(World &w, Solver &S, float dt) {
+HK_DEV void solve_islands(World &w, Solver &S, float dt, int ablate) {
   const float h = dt;
   const int seed_order[3] = {B_PK, B_P2, B_P1};
   for (int i = 0; i < NB; ++i) w.b[i].island_flag = 0;
@@ -1051,11 +1107,11 @@ HK_DEV void solve_islands(World &w, Solver &S, float dt) {
     solver_init(w, S, icont, nc, 1);
     solver_init_velocity(w, S, P, Vl);
     solver_warm_start(S, Vl);
-    for (int it = 0; it < kVelIters; ++it) solver_solve_velocity(S, Vl);
+    for (int it = 0; it < ((ablate & 1) ? 0 : kVelIters); ++it) solver_solve_velocity(S, Vl);
     solver_store(w, S);
     integrate_positions(h, P, Vl, nb);
     int solved = 0;
-    for (int it = 0; it < kPosIters; ++it) {
+    for (int it = 0; it < ((ablate & 2) ? 1 : kPosIters); ++it) {
       float minSep = solver_position_pass(S, P, 0, 0, 0);
       if (minSep >= -3.0f * kLinearSlop) { solved = 1; break; }
     }
@@ -1095,7 +1151,11 @@ HK_DEV void body_advance(Body &b, float alpha) {
   b.xf.p = vsub(b.c, mul_rv(b.xf.q, b.lc));
 }
 
-HK_DEV void solve_toi(World &w, Solver &S, float dt) {
+// register-resident mini-island solver (hk_fast.h)
+HK_DEV void fast_toi_island(World &w, const int *icont, int nc, int toiA, int toiB, float sub_dt, const int *ibodies,
+                            int nb);
+
+HK_DEV void solve_toi(World &w, Solver &S, float dt, int ablate, PhaseT &T) {
   for (int i = 0; i < NB; ++i) { w.b[i].island_flag = 0; w.b[i].alpha0 = 0.0f; }
   for (int p = 0; p < NP; ++p) {
     w.c[p].toi_flag = 0; w.c[p].island_flag = 0; w.c[p].toi_count = 0; w.c[p].toi = 1.0f;
@@ -1126,16 +1186,21 @@ HK_DEV void solve_toi(World &w, Solver &S, float dt) {
           alpha0 = bA.alpha0;
           Sweep s = body_sweep(bB); sweep_advance(s, alpha0); body_set_sweep(bB, s);
         }
-        Proxy pA = make_proxy(SC.fx[SC.pairA[p]]), pB = make_proxy(SC.fx[SC.pairB[p]]);
-        float beta;
-        int st = time_of_impact(pA, pB, body_sweep(bA), body_sweep(bB), 1.0f, beta);
-        if (st == TOI_TOUCHING) alpha = fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f);
-        else alpha = 1.0f;
+        if (pair_far_toi(w, p)) {
+          alpha = 1.0f;
+        } else {
+          Proxy pA = make_proxy(SC.fx[SC.pairA[p]]), pB = make_proxy(SC.fx[SC.pairB[p]]);
+          float beta;
+          int st = time_of_impact(pA, pB, body_sweep(bA), body_sweep(bB), 1.0f, beta);
+          if (st == TOI_TOUCHING) alpha = fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f);
+          else alpha = 1.0f;
+        }
         c.toi = alpha;
         c.toi_flag = 1;
       }
       if (alpha < minAlpha) { minc = p; minAlpha = alpha; }
     }
+    HK_TIC(T, 6);
     if (minc < 0 || 1.0f - 10.0f * kFltEps < minAlpha) break;
     Contact &mc = w.c[minc];
     const int iA_ = SC.pbodyA[minc], iB_ = SC.pbodyB[minc];
@@ -1179,7 +1244,7 @@ HK_DEV void solve_toi(World &w, Solver &S, float dt) {
         if (SC.sensor[e]) continue;
         Sweep backup = body_sweep(ob);
         if (!ob.island_flag) body_advance(ob, minAlpha);
-        contact_update(w, e);
+        contact_update_any(w, e);
         if (!c.enabled || !c.touching) {
           body_set_sweep(ob, backup);
           synchronize_transform(ob);
@@ -1195,6 +1260,11 @@ HK_DEV void solve_toi(World &w, Solver &S, float dt) {
     }
     if (nc > kMaxIsland) { w.overflow = 1; nc = kMaxIsland; }
     const float sub_dt = (1.0f - minAlpha) * dt;
+    HK_TIC(T, 4);
+    if (nc <= 3) {
+      fast_toi_island(w, icont, nc, iA_, iB_, sub_dt, ibodies, nb);
+      HK_TIC(T, 7);
+    } else {
     PosV P[NB];
     VelV Vl[NB];
     for (int i = 0; i < nb; ++i) {
@@ -1211,13 +1281,14 @@ HK_DEV void solve_toi(World &w, Solver &S, float dt) {
     bB.c0 = P[bB.island_index].c;
     bB.a0 = P[bB.island_index].a;
     solver_init_velocity(w, S, P, Vl);
-    for (int it = 0; it < kVelIters; ++it) solver_solve_velocity(S, Vl);
+    for (int it = 0; it < ((ablate & 1) ? 0 : kVelIters); ++it) solver_solve_velocity(S, Vl);
     integrate_positions(sub_dt, P, Vl, nb);
     for (int i = 0; i < nb; ++i) {
       Body &b = w.b[ibodies[i]];
       b.c = P[i].c; b.a = P[i].a; b.v = Vl[i].v; b.w = Vl[i].w;
       synchronize_transform(b);
     }
+    }  // generic path
     for (int i = 0; i < nb; ++i) {
       Body &b = w.b[ibodies[i]];
       b.island_flag = 0;
@@ -1229,14 +1300,6 @@ HK_DEV void solve_toi(World &w, Solver &S, float dt) {
       }
     }
   }
-}
-
-HK_DEV void world_step(World &w, Solver &S) {
-  const float dt = 0.02f;
-  collide(w);
-  solve_islands(w, S, dt);
-  solve_toi(w, S, dt);
-  for (int i = 0; i < 3; ++i) { w.b[i].force = V(0.0f, 0.0f); w.b[i].torque = 0.0f; }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -9,10 +9,10 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libhockey_hip.so")
+LIB_PATH = os.environ.get("HK_LIB") or os.path.join(_HERE, "_lib", "libhockey_hip.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
-OBS_DIM, ACT_DIM, INFO_DIM, STATE_DIM, AUX_DIM, PARAM_DIM, DEBUG_DIM, NUM_COUNTERS = 18, 8, 4, 18, 5, 6, 13, 8
+OBS_DIM, ACT_DIM, INFO_DIM, STATE_DIM, AUX_DIM, PARAM_DIM, DEBUG_DIM, NUM_COUNTERS = 18, 8, 4, 18, 5, 6, 13, 16
 
 POLICY_EXTERNAL, POLICY_RANDOM, POLICY_BASIC_WEAK, POLICY_BASIC_STRONG = 0, 1, 2, 3
 STEP_SKIP_PHYSICS = 1

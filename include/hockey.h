@@ -33,7 +33,7 @@ extern "C" {
 #define HK_AUX_DIM 5    /* has_puck1, has_puck2, time, done, winner */
 #define HK_PARAM_DIM 6  /* reset placement: p2x, p2y, puckx, pucky, puck_fx, puck_fy */
 #define HK_DEBUG_DIM 13 /* pre-solve F1xy, F2xy, Fpuck xy, tau1, tau2, ldamp1,2,puck, adamp1,2 */
-#define HK_NUM_COUNTERS 8
+#define HK_NUM_COUNTERS 16
 
 enum {
   HK_OK = 0,

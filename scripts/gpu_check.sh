@@ -13,12 +13,12 @@ ok $rc || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 $OUT/smoke.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 ${T_BENCH:-600} python bench.py --steps ${BENCH_STEPS:-100} --warmup 10 ${BENCH_ARGS:-} > $OUT/bench.log 2>&1
+timeout -k 10 ${T_BENCH:-600} python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 $OUT/bench.log
 [ $rc -eq 0 ] || exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-    python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
+    python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 $OUT/prof.log
   find $OUT/prof -name "*stats*" | head
 fi
