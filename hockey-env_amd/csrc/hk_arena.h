@@ -1,0 +1,886 @@
+// hk_arena.h -- one arena per lane, register-resident (v3 of the step kernel).
+//
+// Reference mapping (hockey/hockey_env.py; Box2D 2.3 for world.Step, restated by the CPU test oracle):
+//   presolve()        HockeyEnv.step pre-solve half :659-680 (translation :436-470, boundaries :420-434,
+//                     rotation :472-483, puck damping :610-616, hold :618-620, shoot :622-633)
+//   world_step()      world.Step(0.02, 180, 60) :682 = Collide -> Solve -> SolveTOI -> ClearForces
+//   begin_contact()   ContactDetector.BeginContact :44-76
+//   observe*/info*    _get_obs :485-498, obs_agent_two :500-516, _get_info :542-566,
+//                     get_info_agent_two :568-591, rewards :518-540
+//   basic_opponent()  BasicOpponent.act :787-833
+//
+// State layout per lane:
+//   * the 3 dynamic bodies live in register arrays (Dyn), indexed with compile-time indices or through
+//     3-way selects for a runtime body id; static bodies are compile-time scene data (__constant__);
+//   * contact state is bitmasks over the 27-pair table (touching / enabled / TOI / island flags);
+//   * Box2D manifolds stay in HBM (DevState::man, [slot][field][arena], lane-contiguous) and are read
+//     or written in place where Box2D reads or writes them;
+//   * per-pair TOI alphas / sub-step counts and the static bodies' sweep alpha0 live in LDS
+//     ([k][64 lanes], conflict-free for any k);
+//   * pair loops are uniform across the wave, so scene data arrives through scalar loads.
+// Nothing in the step touches private (scratch) memory.  Float operation order is the oracle's.
+#pragma once
+#include "hk_geom.h"
+#include "hk_kernels.h"
+
+namespace hk {
+
+#define SC g_scene
+
+constexpr int kFastC = 3;         // register-resident solver slots (covers ~99.98% of island solves)
+constexpr int kBigC = kMaxIsland;  // generic solver bound (geometric max is 9)
+constexpr uint32_t kEdgeMask[3] = {(1u << 8) | (1u << 10) | (0xFFu << 11),   // player1: 8, 10, 11..18
+                                   (1u << 9) | (1u << 10) | (0xFFu << 19),   // player2: 9, 10, 19..26
+                                   0x3FFu};                                  // puck: 0..9
+constexpr uint32_t kSensorMask = (1u << 6) | (1u << 7);
+
+// LDS per lane: [0,27) TOI alpha per pair, [27,35) static sweep alpha0, [35,62) TOI sub-step count
+constexpr int kLdsToi = 0, kLdsSal0 = 27, kLdsCnt = 35, kLdsPerLane = 62;
+
+struct Dyn {
+  float px[3], py[3], qs[3], qc[3];      // transform (origin, rotation)
+  float cx[3], cy[3], a[3];              // sweep c, a (COM, angle)
+  float c0x[3], c0y[3], a0[3], al0[3];   // sweep c0, a0, alpha0
+  float vx[3], vy[3], w[3];
+  float fx[3], fy[3], tq[3];
+  float ld[3], ad[3], sleep[3];
+  int awake[3];
+};
+
+struct Arena {
+  Dyn d;
+  uint32_t touch, enabled, toiflag, cisl, bisl;
+  int keep_mode, max_t, time, done, winner, has1, has2, vel_ref;
+  int force_big;  // diagnostics: always take the generic (large-island) solver
+  int n_toi, overflow, n_big;  // TOI events, island overflow flag, large-island (generic) solves
+  float *man;   // HBM manifolds
+  float *ws;    // HBM slot workspace of large islands (HbmSlots)
+  int64_t n, a;
+  float *lds;   // this wave's LDS block
+  int lane;
+#ifdef HK_TRACE
+  float *trace;  // diagnostic build: per-phase snapshots (HK_TRACE_POINT)
+#endif
+};
+
+// Diagnostic build only (make TRACE=1): snapshot the arena after phase k into io.debug[a][13 + 24k ...].
+#ifdef HK_TRACE
+constexpr int kTraceStride = 13 + 24 * 4 + 128;
+HK_DEV void trace_point(const Arena &w, int k) {
+  if (!w.trace) return;
+  float *t = w.trace + 13 + 24 * k;
+  for (int b = 0; b < 3; ++b) {
+    t[6 * b + 0] = w.d.px[b]; t[6 * b + 1] = w.d.py[b]; t[6 * b + 2] = w.d.a[b];
+    t[6 * b + 3] = w.d.vx[b]; t[6 * b + 4] = w.d.vy[b]; t[6 * b + 5] = w.d.w[b];
+  }
+  t[18] = __int_as_float((int)w.touch);
+  t[19] = __int_as_float((int)w.enabled);
+  t[20] = __int_as_float(w.d.awake[0] | (w.d.awake[1] << 1) | (w.d.awake[2] << 2));
+  t[21] = (float)w.n_toi;
+  t[22] = (float)w.n_big;
+  t[23] = __int_as_float((int)w.cisl);
+}
+#define HK_TRACE_POINT(w, k) trace_point(w, k)
+#define HK_TRACE_SLOT(w, k, s)                                              \
+  do {                                                                      \
+    if ((w).trace) {                                                        \
+      const float *_src = reinterpret_cast<const float *>(&(s));            \
+      for (int _q = 0; _q < 64 && _q < (int)(sizeof(s) / 4); ++_q)          \
+        (w).trace[13 + 96 + 64 * (k) + _q] = _src[_q];                      \
+    }                                                                       \
+  } while (0)
+#else
+#define HK_TRACE_SLOT(w, k, s) ((void)0)
+#define HK_TRACE_POINT(w, k) ((void)0)
+#endif
+
+// ------------------------------------------------------------------------------------------------
+// runtime-id access to the register body file (3-way selects, static -> default)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+HK_DEV T pick(const T (&x)[3], int b, T dflt) {
+  return b == 0 ? x[0] : (b == 1 ? x[1] : (b == 2 ? x[2] : dflt));
+}
+template <typename T>
+HK_DEV void place(T (&x)[3], int b, T v) {
+  x[0] = b == 0 ? v : x[0];
+  x[1] = b == 1 ? v : x[1];
+  x[2] = b == 2 ? v : x[2];
+}
+HK_DEV float &LDS(Arena &w, int k) { return w.lds[k * 64 + w.lane]; }
+HK_DEV float &MF(const Arena &w, int slot, int field) { return w.man[((int64_t)slot * NMF + field) * w.n + w.a]; }
+
+HK_DEV float inv_mass(int b) { return b < 3 ? SC.invMass[b] : 0.0f; }
+HK_DEV float inv_inertia(int b) { return b < 3 ? SC.invI[b] : 0.0f; }
+HK_DEV v2 local_center(int b) { return b < 3 ? V(SC.lcx[b], SC.lcy[b]) : V(0.0f, 0.0f); }
+
+HK_DEV xform body_xf(const Arena &w, int b) {
+  xform x;
+  if (b < 3) {
+    x.p = V(pick(w.d.px, b, 0.0f), pick(w.d.py, b, 0.0f));
+    x.q.s = pick(w.d.qs, b, 0.0f);
+    x.q.c = pick(w.d.qc, b, 1.0f);
+  } else {
+    x.p = V(SC.spx[b], SC.spy[b]);
+    x.q.s = 0.0f;  // rot_set(0) == (+0, 1)
+    x.q.c = 1.0f;
+  }
+  return x;
+}
+HK_DEV v2 body_c(const Arena &w, int b) {
+  return b < 3 ? V(pick(w.d.cx, b, 0.0f), pick(w.d.cy, b, 0.0f)) : V(SC.spx[b], SC.spy[b]);
+}
+HK_DEV Sweep body_sweep(Arena &w, int b) {
+  Sweep s;
+  if (b < 3) {
+    s.lc = local_center(b);
+    s.c0 = V(pick(w.d.c0x, b, 0.0f), pick(w.d.c0y, b, 0.0f));
+    s.c = V(pick(w.d.cx, b, 0.0f), pick(w.d.cy, b, 0.0f));
+    s.a0 = pick(w.d.a0, b, 0.0f);
+    s.a = pick(w.d.a, b, 0.0f);
+    s.alpha0 = pick(w.d.al0, b, 0.0f);
+  } else {  // static: c0 == c == origin and a0 == a == 0 forever; only alpha0 moves (b2Sweep::Advance)
+    s.lc = V(0.0f, 0.0f);
+    s.c0 = s.c = V(SC.spx[b], SC.spy[b]);
+    s.a0 = s.a = 0.0f;
+    s.alpha0 = LDS(w, kLdsSal0 + b - 3);
+  }
+  return s;
+}
+HK_DEV void body_set_sweep(Arena &w, int b, const Sweep &s) {
+  if (b < 3) {
+    place(w.d.c0x, b, s.c0.x);
+    place(w.d.c0y, b, s.c0.y);
+    place(w.d.cx, b, s.c.x);
+    place(w.d.cy, b, s.c.y);
+    place(w.d.a0, b, s.a0);
+    place(w.d.a, b, s.a);
+    place(w.d.al0, b, s.alpha0);
+  } else {
+    LDS(w, kLdsSal0 + b - 3) = s.alpha0;
+  }
+}
+// b2Body::SynchronizeTransform
+HK_DEV void sync_xf(Arena &w, int b) {
+  if (b >= 3) return;  // a static transform is its origin (c - R(0) * 0 == c exactly)
+  const float a = pick(w.d.a, b, 0.0f);
+  const rot q = rot_set(a);
+  const v2 p = vsub(V(pick(w.d.cx, b, 0.0f), pick(w.d.cy, b, 0.0f)), mul_rv(q, local_center(b)));
+  place(w.d.qs, b, q.s);
+  place(w.d.qc, b, q.c);
+  place(w.d.px, b, p.x);
+  place(w.d.py, b, p.y);
+}
+// b2Body::SetAwake (dynamic bodies only; a static body has no awake state that matters here)
+HK_DEV void set_awake(Arena &w, int b, int flag) {
+  if (b >= 3) return;
+  if (flag) {
+    if (!pick(w.d.awake, b, 1)) {
+      place(w.d.awake, b, 1);
+      place(w.d.sleep, b, 0.0f);
+    }
+  } else {
+    place(w.d.awake, b, 0);
+    place(w.d.sleep, b, 0.0f);
+    place(w.d.vx, b, 0.0f);
+    place(w.d.vy, b, 0.0f);
+    place(w.d.w, b, 0.0f);
+    place(w.d.fx, b, 0.0f);
+    place(w.d.fy, b, 0.0f);
+    place(w.d.tq, b, 0.0f);
+  }
+}
+// b2Body::Advance
+HK_DEV void body_advance(Arena &w, int b, float alpha) {
+  Sweep s = body_sweep(w, b);
+  sweep_advance(s, alpha);
+  s.c = s.c0;
+  s.a = s.a0;
+  body_set_sweep(w, b, s);
+  sync_xf(w, b);
+}
+
+// compile-time body helpers (b2Body setters used by the env laws)
+template <int B>
+HK_DEV void set_transform(Arena &w, v2 p, float angle) {
+  const rot q = rot_set(angle);
+  w.d.qs[B] = q.s;
+  w.d.qc[B] = q.c;
+  w.d.px[B] = p.x;
+  w.d.py[B] = p.y;
+  xform x;
+  x.p = p;
+  x.q = q;
+  const v2 c = mul_xv(x, V(SC.lcx[B], SC.lcy[B]));
+  w.d.cx[B] = c.x;
+  w.d.cy[B] = c.y;
+  w.d.a[B] = angle;
+  w.d.c0x[B] = c.x;
+  w.d.c0y[B] = c.y;
+  w.d.a0[B] = angle;
+}
+template <int B>
+HK_DEV void wake(Arena &w) {
+  if (!w.d.awake[B]) { w.d.awake[B] = 1; w.d.sleep[B] = 0.0f; }
+}
+template <int B>
+HK_DEV void set_linear_velocity(Arena &w, v2 v) {
+  if (dot(v, v) > 0.0f) wake<B>(w);
+  w.d.vx[B] = v.x;
+  w.d.vy[B] = v.y;
+}
+template <int B>
+HK_DEV void set_angular_velocity(Arena &w, float om) {
+  if (om * om > 0.0f) wake<B>(w);
+  w.d.w[B] = om;
+}
+template <int B>
+HK_DEV void apply_force(Arena &w, v2 f) {
+  wake<B>(w);
+  w.d.fx[B] = w.d.fx[B] + f.x;
+  w.d.fy[B] = w.d.fy[B] + f.y;
+}
+template <int B>
+HK_DEV void apply_torque(Arena &w, float t) {
+  wake<B>(w);
+  w.d.tq[B] += t;
+}
+
+// ------------------------------------------------------------------------------------------------
+// lane-local broad phase (exact outcome-preserving rejection)
+//   Box2D clipping emits points up to sqrt(2) * totalRadius from the reference polygon and the circle
+//   manifold up to totalRadius: reach = 2 * (rA + rB); every TOI "touching" exit needs the core
+//   distance below target + tol < rA + rB at some t.
+// ------------------------------------------------------------------------------------------------
+HK_DEV float box_gap(float ax0, float ay0, float ax1, float ay1, const float *b) {
+  return fmaxf(fmaxf(b[0] - ax1, ax0 - b[2]), fmaxf(b[1] - ay1, ay0 - b[3]));
+}
+HK_DEV bool pair_far_collide(const Arena &w, int p) {
+  const int fA = SC.pairA[p], fB = SC.pairB[p], bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
+  const v2 cB = body_c(w, bB);
+  const float rB = SC.rcore[bB];
+  if (bA >= 3) return box_gap(cB.x - rB, cB.y - rB, cB.x + rB, cB.y + rB, SC.fx_aabb[fA]) > reach;
+  const v2 cA = body_c(w, bA);
+  const float lim = SC.rcore[bA] + rB + reach;
+  const float dx = cA.x - cB.x, dy = cA.y - cB.y;
+  return dx * dx + dy * dy > lim * lim;
+}
+HK_DEV bool pair_far_toi(const Arena &w, int p) {  // static A, dynamic B, sweeps already aligned
+  const int fA = SC.pairA[p], fB = SC.pairB[p], bB = SC.pbodyB[p];
+  const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
+  const float r = SC.rcore[bB];
+  const float c0x = pick(w.d.c0x, bB, 0.0f), c0y = pick(w.d.c0y, bB, 0.0f);
+  const float cx = pick(w.d.cx, bB, 0.0f), cy = pick(w.d.cy, bB, 0.0f);
+  return box_gap(fminf(c0x, cx) - r, fminf(c0y, cy) - r, fmaxf(c0x, cx) + r, fmaxf(c0y, cy) + r,
+                 SC.fx_aabb[fA]) > reach;
+}
+
+// ------------------------------------------------------------------------------------------------
+// ContactDetector.BeginContact (hockey_env.py:44-76) and b2Contact::Update
+// ------------------------------------------------------------------------------------------------
+HK_DEV void begin_contact(Arena &w, int p) {
+  const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const int hasPK = (bA == B_PK || bB == B_PK);
+  if ((bA == B_G2 || bB == B_G2) && hasPK) { w.done = 1; w.winner = 1; }
+  if ((bA == B_G1 || bB == B_G1) && hasPK) { w.done = 1; w.winner = -1; }
+  if ((bA == B_P1 || bB == B_P1) && hasPK) {
+    if (w.keep_mode && (double)w.d.vx[B_PK] < 0.1)
+      if (w.has1 == 0) w.has1 = 15;
+  }
+  if ((bA == B_P2 || bB == B_P2) && hasPK) {
+    if (w.keep_mode && (double)w.d.vx[B_PK] > -0.1)
+      if (w.has2 == 0) w.has2 = 15;
+  }
+}
+
+HK_DEV void pair_update(Arena &w, int p) {
+  const int fA = SC.pairA[p], fB = SC.pairB[p], bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const uint32_t bit = 1u << p;
+  const int was = (w.touch & bit) != 0u;
+  w.enabled |= bit;
+  int touching;
+  if (pair_far_collide(w, p)) {
+    touching = 0;
+    if (!SC.sensor[p] && was) { set_awake(w, bA, 1); set_awake(w, bB, 1); }
+  } else {
+    const xform xA = body_xf(w, bA), xB = body_xf(w, bB);
+    if (SC.sensor[p]) {
+      touching = test_overlap(SC.fx[fA], xA, SC.fx[fB], xB);
+    } else {
+      Manifold m;
+      if (SC.fx[fB].circle) collide_poly_circle(m, SC.fx[fA], xA, SC.fx[fB], xB);
+      else collide_polygons(m, SC.fx[fA], xA, SC.fx[fB], xB);
+      touching = m.count > 0;
+      if (touching) {
+        const int slot = SC.manslot[p];
+        // match old contact ids to carry impulses (the stored manifold is meaningful only if touching)
+        int oc = 0;
+        uint32_t oid0 = 0u, oid1 = 0u;
+        float oni0 = 0.0f, oni1 = 0.0f, oti0 = 0.0f, oti1 = 0.0f;
+        if (was) {
+          oc = __float_as_int(MF(w, slot, M_META)) & 0xff;
+          oid0 = (uint32_t)__float_as_int(MF(w, slot, M_P0ID));
+          oni0 = MF(w, slot, M_P0NI);
+          oti0 = MF(w, slot, M_P0TI);
+          oid1 = (uint32_t)__float_as_int(MF(w, slot, M_P1ID));
+          oni1 = MF(w, slot, M_P1NI);
+          oti1 = MF(w, slot, M_P1TI);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (i < m.count) {
+            m.ni[i] = 0.0f;
+            m.ti[i] = 0.0f;
+            if (oc > 0 && oid0 == m.id[i]) { m.ni[i] = oni0; m.ti[i] = oti0; }
+            else if (oc > 1 && oid1 == m.id[i]) { m.ni[i] = oni1; m.ti[i] = oti1; }
+          }
+        }
+        MF(w, slot, M_META) = __int_as_float(m.count | (m.type << 8));
+        MF(w, slot, M_LNX) = m.ln.x;
+        MF(w, slot, M_LNY) = m.ln.y;
+        MF(w, slot, M_LPX) = m.lp.x;
+        MF(w, slot, M_LPY) = m.lp.y;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (j < m.count) {
+            const int o = M_P0X + j * 5;
+            MF(w, slot, o + 0) = m.pt_lp[j].x;
+            MF(w, slot, o + 1) = m.pt_lp[j].y;
+            MF(w, slot, o + 2) = __int_as_float((int)m.id[j]);
+            MF(w, slot, o + 3) = m.ni[j];
+            MF(w, slot, o + 4) = m.ti[j];
+          }
+        }
+      }
+      if (touching != was) { set_awake(w, bA, 1); set_awake(w, bB, 1); }
+    }
+  }
+  w.touch = touching ? (w.touch | bit) : (w.touch & ~bit);
+  if (!was && touching) begin_contact(w, p);
+}
+
+// b2ContactManager::Collide
+HK_DEV void collide(Arena &w) {
+  for (int p = 0; p < NP; ++p) {
+    const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+    const int activeA = bA < 3 && pick(w.d.awake, bA, 0);
+    const int activeB = pick(w.d.awake, bB, 0);
+    if (!activeA && !activeB) continue;
+    pair_update(w, p);
+  }
+}
+
+}  // namespace hk
+
+#include "hk_solver.h"
+
+namespace hk {
+
+// ------------------------------------------------------------------------------------------------
+// b2World::Solve: islands by DFS (Box2D's seed order and edge order), solved together (they share no
+// dynamic body), position early exit and sleep per island.
+// ------------------------------------------------------------------------------------------------
+template <typename SL>
+HK_DEV bool solve_islands(Arena &w, SL &S, float dt) {
+  constexpr int MAXS = SlotCap<SL>::value;
+  const float h = dt;
+  int island_of[3] = {-1, -1, -1};
+  int nc = 0, nisl = 0;
+  uint32_t inis = 0u;
+  const uint32_t live = w.enabled & w.touch & ~kSensorMask;
+  const int seed_order[3] = {B_PK, B_P2, B_P1};
+#pragma unroll
+  for (int si = 0; si < 3; ++si) {
+    const int seed = seed_order[si];
+    if (island_of[seed] >= 0 || !w.d.awake[seed]) continue;
+    const int isl = nisl++;
+    int st0 = seed, st1 = 0, st2 = 0, sc = 1;  // DFS stack of dynamic bodies (statics never propagate)
+    island_of[seed] = isl;
+    while (sc > 0) {
+      const int bi = sc == 3 ? st2 : (sc == 2 ? st1 : st0);
+      --sc;
+      set_awake(w, bi, 1);
+      uint32_t m = pick(kEdgeMask, bi, 0u) & live & ~inis;
+      while (m) {
+        const int e = __ffs(m) - 1;
+        m &= m - 1u;
+        inis |= 1u << e;
+        S.set_pair(nc, e, isl);
+        ++nc;
+        const int pa = SC.pbodyA[e], pb = SC.pbodyB[e];
+        const int other = pa == bi ? pb : pa;
+        if (other >= 3) continue;
+        if (pick(island_of, other, 0) >= 0) continue;
+        place(island_of, other, isl);
+        if (sc == 0) st0 = other; else if (sc == 1) st1 = other; else st2 = other;
+        ++sc;
+      }
+    }
+  }
+  if (nc > MAXS) return false;
+  // integrate velocities (b2Island::Solve), in place in the register body file
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    if (island_of[b] >= 0) {
+      w.d.c0x[b] = w.d.cx[b];
+      w.d.c0y[b] = w.d.cy[b];
+      w.d.a0[b] = w.d.a[b];
+      v2 v = V(w.d.vx[b], w.d.vy[b]);
+      float wv = w.d.w[b];
+      v = vadd(v, vs(h, vadd(vs(1.0f, V(0.0f, 0.0f)), vs(SC.invMass[b], V(w.d.fx[b], w.d.fy[b])))));
+      wv += h * SC.invI[b] * w.d.tq[b];
+      v = vs(1.0f / (1.0f + h * w.d.ld[b]), v);
+      wv *= 1.0f / (1.0f + h * w.d.ad[b]);
+      w.d.vx[b] = v.x;
+      w.d.vy[b] = v.y;
+      w.d.w[b] = wv;
+    }
+  }
+  HK_TRACE_POINT(w, 3);
+  S.each(nc, [&](FSlot &s, int) {
+    fslot_load(s, w, s.p, 1, s.isl);
+    fslot_init_velocity(s, w.d);
+  });
+  S.each(nc, [&](FSlot &s, int) { fslot_warm_start(s, w.d); });
+  velocity_iterations(S, w.d, nc);
+  S.each(nc, [&](FSlot &s, int) { fslot_store(s, w); });
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    if (island_of[b] >= 0) integrate_one(h, w.d, b);
+  int solved = 0;
+  const int all = (1 << nisl) - 1;
+  for (int it = 0; it < kPosIters && (solved & all) != all; ++it) {
+    float ms0 = 0.0f, ms1 = 0.0f, ms2 = 0.0f;
+    S.each(nc, [&](FSlot &s, int) {
+      if (!((solved >> s.isl) & 1)) {
+        const float m = fslot_solve_position(s, w.d, kBaumgarte, s.mA, s.iA, s.mB, s.iB, 0.0f);
+        ms0 = s.isl == 0 ? fmin2(ms0, m) : ms0;
+        ms1 = s.isl == 1 ? fmin2(ms1, m) : ms1;
+        ms2 = s.isl == 2 ? fmin2(ms2, m) : ms2;
+      }
+    });
+    if (ms0 >= -3.0f * kLinearSlop) solved |= 1;
+    if (ms1 >= -3.0f * kLinearSlop) solved |= 2;
+    if (ms2 >= -3.0f * kLinearSlop) solved |= 4;
+  }
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    if (island_of[b] >= 0) sync_xf(w, b);
+  const float linTolSqr = kLinearSleepTol * kLinearSleepTol;
+  const float angTolSqr = kAngularSleepTol * kAngularSleepTol;
+  for (int isl = 0; isl < nisl; ++isl) {
+    float minSleep = kFltMax;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      if (island_of[b] == isl) {
+        if (w.d.w[b] * w.d.w[b] > angTolSqr || w.d.vx[b] * w.d.vx[b] + w.d.vy[b] * w.d.vy[b] > linTolSqr) {
+          w.d.sleep[b] = 0.0f;
+          minSleep = 0.0f;
+        } else {
+          w.d.sleep[b] += h;
+          minSleep = fmin2(minSleep, w.d.sleep[b]);
+        }
+      }
+    }
+    if (minSleep >= kTimeToSleep && ((solved >> isl) & 1)) {
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+        if (island_of[b] == isl) set_awake(w, b, 0);
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// b2World::SolveTOI.  In this scene a TOI pair is always (static A, dynamic B), so the mini-island
+// holds exactly one dynamic body: B plus its touching static contacts (minContact first, then B's
+// contact edges in order).  Mass gating of SolveTOIPositionConstraints is therefore the identity.
+// ------------------------------------------------------------------------------------------------
+template <typename SL>
+HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, int db, float sub_dt) {
+  uint32_t m = extra;
+  S.each(nc, [&](FSlot &s, int i) {
+    int p = minc;
+    if (i > 0) { p = __ffs(m) - 1; m &= m - 1u; }
+    fslot_load(s, w, p, 0, 0);
+  });
+  for (int it = 0; it < 20; ++it) {
+    float minSep = 0.0f;
+    S.each(nc, [&](FSlot &s, int) {
+      minSep = fslot_solve_position(s, w.d, kToiBaumgarte, s.mA, s.iA, s.mB, s.iB, minSep);
+    });
+    if (minSep >= -1.5f * kLinearSlop) break;
+  }
+  // leap of faith (the static body's c0 already equals its c)
+  place(w.d.c0x, db, pick(w.d.cx, db, 0.0f));
+  place(w.d.c0y, db, pick(w.d.cy, db, 0.0f));
+  place(w.d.a0, db, pick(w.d.a, db, 0.0f));
+  S.each(nc, [&](FSlot &s, int) { fslot_init_velocity(s, w.d); });
+  velocity_iterations(S, w.d, nc);
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    if (b == db) integrate_one(sub_dt, w.d, b);
+  sync_xf(w, db);
+}
+
+HK_DEV void solve_toi(Arena &w, float dt) {
+#pragma unroll
+  for (int b = 0; b < 3; ++b) w.d.al0[b] = 0.0f;
+  for (int k = 0; k < 8; ++k) LDS(w, kLdsSal0 + k) = 0.0f;
+  for (int p = 0; p < NP; ++p) {
+    LDS(w, kLdsToi + p) = 1.0f;
+    LDS(w, kLdsCnt + p) = 0.0f;
+  }
+  w.toiflag = 0u;
+  w.cisl = 0u;
+  w.bisl = 0u;
+  for (;;) {
+    int minc = -1;
+    float minAlpha = 1.0f;
+    for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
+      const uint32_t bit = 1u << p;
+      if (!(w.enabled & bit)) continue;
+      if (LDS(w, kLdsCnt + p) > (float)kMaxSubSteps) continue;
+      float alpha = 1.0f;
+      if (w.toiflag & bit) {
+        alpha = LDS(w, kLdsToi + p);
+      } else {
+        if (SC.sensor[p]) continue;
+        const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+        if (bA < 3) continue;                 // dynamic-dynamic, non-bullet: no continuous collision
+        if (!pick(w.d.awake, bB, 0)) continue;  // static A is never active
+        float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
+        float alpha0 = a0A;
+        if (a0A < a0B) {
+          alpha0 = a0B;
+          LDS(w, kLdsSal0 + bA - 3) = a0B;  // static b2Sweep::Advance: only alpha0 moves
+        } else if (a0B < a0A) {
+          alpha0 = a0A;
+          Sweep s = body_sweep(w, bB);
+          sweep_advance(s, alpha0);
+          body_set_sweep(w, bB, s);
+        }
+        if (pair_far_toi(w, p)) {
+          alpha = 1.0f;
+        } else {
+          const Proxy pA = make_proxy(SC.fx[SC.pairA[p]]), pB = make_proxy(SC.fx[SC.pairB[p]]);
+          float beta;
+          const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);
+          alpha = st == TOI_TOUCHING ? fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f) : 1.0f;
+        }
+        LDS(w, kLdsToi + p) = alpha;
+        w.toiflag |= bit;
+      }
+      if (alpha < minAlpha) { minc = p; minAlpha = alpha; }
+    }
+    if (minc < 0 || 1.0f - 10.0f * kFltEps < minAlpha) break;
+    // ---- one TOI event (per-lane pair) ----
+    const int bA = SC.pbodyA[minc], bB = SC.pbodyB[minc];  // static A, dynamic B
+    const uint32_t mbit = 1u << minc;
+    const Sweep backA = body_sweep(w, bA), backB = body_sweep(w, bB);
+    body_advance(w, bA, minAlpha);
+    body_advance(w, bB, minAlpha);
+    pair_update(w, minc);
+    w.toiflag &= ~mbit;
+    LDS(w, kLdsCnt + minc) += 1.0f;
+    if (!(w.enabled & mbit) || !(w.touch & mbit)) {
+      w.enabled &= ~mbit;
+      body_set_sweep(w, bA, backA);
+      body_set_sweep(w, bB, backB);
+      sync_xf(w, bA);
+      sync_xf(w, bB);
+      continue;
+    }
+    w.n_toi++;
+    set_awake(w, bA, 1);
+    set_awake(w, bB, 1);
+    w.bisl = (1u << bA) | (1u << bB);
+    w.cisl |= mbit;
+    uint32_t extra = 0u;  // other island contacts, added in B's (ascending) edge order
+    int nc = 1;
+    uint32_t m = pick(kEdgeMask, bB, 0u) & ~kSensorMask;
+    while (m) {
+      const int e = __ffs(m) - 1;
+      m &= m - 1u;
+      const uint32_t ebit = 1u << e;
+      if (w.cisl & ebit) continue;
+      const int other = SC.pbodyA[e] == bB ? SC.pbodyB[e] : SC.pbodyA[e];
+      if (other < 3) continue;  // only static bodies join a TOI island
+      const Sweep backup = body_sweep(w, other);
+      if (!((w.bisl >> other) & 1u)) body_advance(w, other, minAlpha);
+      pair_update(w, e);
+      if (!(w.enabled & ebit) || !(w.touch & ebit)) {
+        body_set_sweep(w, other, backup);
+        continue;
+      }
+      w.cisl |= ebit;
+      extra |= ebit;
+      ++nc;
+      w.bisl |= 1u << other;
+    }
+    const float sub_dt = (1.0f - minAlpha) * dt;
+    if (nc > kBigC) { w.overflow = 1; nc = kBigC; }
+    if (nc <= kFastC && !w.force_big) {
+      RegSlots S;
+      toi_island_solve(w, S, minc, extra, nc, bB, sub_dt);
+    } else {
+      w.n_big++;
+      HbmSlots S{w.ws, w.n, w.a};
+      toi_island_solve(w, S, minc, extra, nc, bB, sub_dt);
+    }
+    // reset island flags; invalidate the TOIs of the displaced dynamic body
+    w.bisl = 0u;
+    const uint32_t em = pick(kEdgeMask, bB, 0u);
+    w.toiflag &= ~em;
+    w.cisl &= ~em;
+  }
+}
+
+// b2World::Step (hockey_env.py:682)
+HK_DEV void world_step(Arena &w, PhaseT &T) {
+  const float dt = 0.02f;
+  collide(w);
+  HK_TIC(T, 2);
+  HK_TRACE_POINT(w, 0);
+  bool done = false;
+  if (!w.force_big) {
+    RegSlots S;
+    done = solve_islands(w, S, dt);
+  }
+  if (!done) {  // more island contacts than register slots: identical solve on the HBM slot file
+    w.n_big++;
+    HbmSlots S{w.ws, w.n, w.a};
+    solve_islands(w, S, dt);
+  }
+  HK_TIC(T, 3);
+  HK_TRACE_POINT(w, 1);
+  solve_toi(w, dt);
+  HK_TIC(T, 4);
+  HK_TRACE_POINT(w, 2);
+#pragma unroll
+  for (int b = 0; b < 3; ++b) { w.d.fx[b] = 0.0f; w.d.fy[b] = 0.0f; w.d.tq[b] = 0.0f; }
+}
+
+// ------------------------------------------------------------------------------------------------
+// HockeyEnv.step laws (hockey_env.py:420-483, 610-633), numpy NEP-50 + pybox2d float32 semantics
+// ------------------------------------------------------------------------------------------------
+constexpr double kDtPy = 0.02;  // self.timeStep = 1.0 / FPS  (hockey_env.py:119)
+constexpr double kPiD = 3.141592653589793;
+
+template <int B>
+HK_DEV void check_boundaries(Arena &w, float &f0, float &f1, int one) {
+  const double px = w.d.px[B], py = w.d.py[B];
+  if ((one && px < 1.5 && f0 < 0) || (!one && px > 8.5 && f0 > 0) || (one && px > 5.0 && f0 > 0) ||
+      (!one && px < 5.0 && f0 < 0)) {
+    float vel0 = w.d.vx[B];
+    if (w.vel_ref) { w.d.vx[B] = 0.0f; vel0 = 0.0f; }
+    f0 = -vel0;
+  }
+  if ((py > 8.0 - 1.2 && f1 > 0) || (py < 1.2 && f1 < 0)) {
+    float vel1 = w.d.vy[B];
+    if (w.vel_ref) { w.d.vy[B] = 0.0f; vel1 = 0.0f; }
+    f1 = -vel1;
+  }
+}
+
+template <int B>
+HK_DEV void translation_law(Arena &w, float a0, float a1) {
+  constexpr int one = (B == B_P1);
+  const double vx = w.d.vx[B], vy = w.d.vy[B];
+  const double speed = sqrt(vx * vx + vy * vy);
+  float f0, f1;
+  if (one) { f0 = a0 * 6000.0f; f1 = a1 * 6000.0f; }
+  else { f0 = (-a0) * 6000.0f; f1 = (-a1) * 6000.0f; }
+  const double px = w.d.px[B], m = SC.mass[B];
+  if ((one && px > 5.0 - 0.5) || (!one && px < 5.0 + 0.5)) {
+    f0 = 0.0f;
+    if (one) {
+      if (vx > 0) f0 = (float)((((-2.0) * vx) * m) / kDtPy);
+      f0 = f0 + (float)(((((-1.0) * (px - 5.0)) * vx) * m) / kDtPy);
+    } else {
+      if (vx < 0) f0 = (float)((((-2.0) * vx) * m) / kDtPy);
+      f0 = f0 + (float)((((1.0 * (px - 5.0)) * vx) * m) / kDtPy);
+    }
+    w.d.ld[B] = 20.0f;
+    check_boundaries<B>(w, f0, f1, one);
+    apply_force<B>(w, V(f0, f1));
+    return;
+  }
+  if (speed < 10.0) {
+    w.d.ld[B] = 5.0f;
+    check_boundaries<B>(w, f0, f1, one);
+    apply_force<B>(w, V(f0, f1));
+  } else {
+    w.d.ld[B] = 20.0f;
+    const float mf = (float)m;
+    const float d0 = (0.02f * f0) / mf, d1 = (0.02f * f1) / mf;
+    const double nx = vx + (double)d0, ny = vy + (double)d1;
+    if (sqrt(nx * nx + ny * ny) < speed) {
+      check_boundaries<B>(w, f0, f1, one);
+      apply_force<B>(w, V(f0, f1));
+    }
+  }
+}
+
+template <int B>
+HK_DEV void rotation_law(Arena &w, float a) {
+  const double ang = w.d.a[B], wv = w.d.w[B], m = SC.mass[B];
+  if (fabs(ang) > kPiD / 3) {
+    double t = 0.0;
+    if (ang * wv > 0) t = (((-0.1) * wv) * m) / kDtPy;
+    t = t + (((-0.1) * ang) * m) / kDtPy;
+    w.d.ad[B] = 10.0f;
+    apply_torque<B>(w, (float)t);
+  } else {
+    w.d.ad[B] = 2.0f;
+    apply_torque<B>(w, a * 400.0f);
+  }
+}
+
+template <int B>
+HK_DEV void shoot(Arena &w) {
+  const double ca = hk_cos((double)w.d.a[B]), sa = hk_sin((double)w.d.a[B]);
+  const double sgn = B == B_P1 ? 1.0 : -1.0;
+  v2 f = V((float)(ca * sgn), (float)(sa * sgn));
+  const float m = SC.mass[B_PK];
+  f = V(f.x * m, f.y * m);
+  f = V(f.x / 0.02f, f.y / 0.02f);
+  f = V(f.x * 60.0f, f.y * 60.0f);
+  apply_force<B_PK>(w, f);
+}
+
+template <int B>
+HK_DEV void keep_puck(Arena &w) {
+  set_transform<B_PK>(w, V(w.d.px[B], w.d.py[B]), w.d.a[B_PK]);
+  set_linear_velocity<B_PK>(w, V(w.d.vx[B], w.d.vy[B]));
+}
+
+HK_DEV float clip1(float x) { return x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x); }
+
+HK_DEV void presolve(Arena &w, const float *a8) {
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = clip1(a8[i]);
+  translation_law<B_P1>(w, a[0], a[1]);
+  rotation_law<B_P1>(w, a[2]);
+  translation_law<B_P2>(w, a[4], a[5]);
+  rotation_law<B_P2>(w, a[6]);
+  {
+    const double vx = w.d.vx[B_PK], vy = w.d.vy[B_PK];
+    const double s = sqrt(vx * vx + vy * vy);
+    w.d.ld[B_PK] = s > 25.0 ? 10.0f : 0.05f;
+  }
+  if (w.keep_mode) {
+    if (w.has1 > 1) {
+      keep_puck<B_P1>(w);
+      w.has1 -= 1;
+      if (w.has1 == 1 || a[3] > 0.5f) { shoot<B_P1>(w); w.has1 = 0; }
+    }
+    if (w.has2 > 1) {
+      keep_puck<B_P2>(w);
+      w.has2 -= 1;
+      if (w.has2 == 1 || a[7] > 0.5f) { shoot<B_P2>(w); w.has2 = 0; }
+    }
+  }
+}
+
+HK_DEV void observe(const Arena &w, float *o) {
+  const Dyn &d = w.d;
+  o[0] = d.px[0] - 5.0f; o[1] = d.py[0] - 4.0f; o[2] = d.a[0];
+  o[3] = d.vx[0]; o[4] = d.vy[0]; o[5] = d.w[0];
+  o[6] = d.px[1] - 5.0f; o[7] = d.py[1] - 4.0f; o[8] = d.a[1];
+  o[9] = d.vx[1]; o[10] = d.vy[1]; o[11] = d.w[1];
+  o[12] = d.px[2] - 5.0f; o[13] = d.py[2] - 4.0f;
+  o[14] = d.vx[2]; o[15] = d.vy[2];
+  o[16] = w.keep_mode ? (float)w.has1 : 0.0f;
+  o[17] = w.keep_mode ? (float)w.has2 : 0.0f;
+}
+
+HK_DEV void observe_two(const Arena &w, float *o) {
+  const Dyn &d = w.d;
+  o[0] = -(d.px[1] - 5.0f); o[1] = -(d.py[1] - 4.0f); o[2] = d.a[1];
+  o[3] = -d.vx[1]; o[4] = -d.vy[1]; o[5] = d.w[1];
+  o[6] = -(d.px[0] - 5.0f); o[7] = -(d.py[0] - 4.0f); o[8] = d.a[0];
+  o[9] = -d.vx[0]; o[10] = -d.vy[0]; o[11] = d.w[0];
+  o[12] = -(d.px[2] - 5.0f); o[13] = -(d.py[2] - 4.0f);
+  o[14] = -d.vx[2]; o[15] = -d.vy[2];
+  o[16] = w.keep_mode ? (float)w.has2 : 0.0f;
+  o[17] = w.keep_mode ? (float)w.has1 : 0.0f;
+}
+
+// _get_info / get_info_agent_two (hockey_env.py:542-591), double like the reference
+template <int TWO>
+HK_DEV void info_side(const Arena &w, double *info4) {
+  constexpr int me = TWO ? B_P2 : B_P1;
+  const Dyn &d = w.d;
+  const double T = (double)w.max_t;
+  double close = 0.0;
+  const int cond = TWO ? ((double)d.px[2] > 5.0 && (double)d.vx[2] >= 0) : ((double)d.px[2] < 5.0 && (double)d.vx[2] <= 0);
+  if (cond) {
+    const float dx = d.px[me] - d.px[2], dy = d.py[me] - d.py[2];
+    const double dd = sqrt((double)dx * (double)dx + (double)dy * (double)dy);
+    const double max_dist = 250.0 / 60.0;
+    const double factor = -30.0 / ((max_dist * T) / 2);
+    close = close + dd * factor;
+  }
+  const double touch = ((TWO ? w.has2 : w.has1) == 15) ? 1.0 : 0.0;
+  const double f2 = TWO ? (-1.0) / (T * 25) : 1.0 / (T * 25);
+  info4[0] = TWO ? -w.winner : w.winner;
+  info4[1] = close;
+  info4[2] = touch;
+  info4[3] = (double)d.vx[2] * f2;
+}
+
+HK_DEV double compute_reward(const Arena &w) {
+  double r = 0;
+  if (w.done) {
+    if (w.winner == 1) r += 10;
+    else if (w.winner != 0) r -= 10;
+  }
+  return r;
+}
+
+// BasicOpponent.act (hockey_env.py:787-833) on an own-frame float32 obs, double arithmetic
+HK_DEV void basic_opponent(int weak, int keep_mode, double &phase, double inc, const float *of, float *act) {
+  const double p1x = of[0], p1y = of[1], p1a = of[2];
+  const double v1[3] = {of[3], of[4], of[5]};
+  const double pkx = of[12], pky = of[13], pvx = of[14], pvy = of[15];
+  double tx, ty;
+  phase += inc;
+  const double kp = weak ? 0.5 : 10.0, kd = 0.5;
+  if (pvx < 30.0 / 60.0) {
+    const double dx = p1x - pkx, dy = p1y - pky;
+    const double dist = sqrt(dx * dx + dy * dy);
+    double ady = p1y - pky;
+    if (ady < 0) ady = -ady;
+    if (p1x < pkx && ady < 30.0 / 60.0) {
+      tx = pkx + 0.2;
+      ty = pky + (pvy * dist) * 0.1;
+    } else {
+      tx = -210.0 / 60.0;
+      ty = pky;
+    }
+  } else {
+    tx = -210.0 / 60.0;
+    ty = 0.0;
+  }
+  const double ta = (kPiD / 3) * hk_sin(phase);
+  const double o16 = of[16];
+  const double shoot_ = (keep_mode && o16 > 0 && o16 < 7) ? 1.0 : 0.0;
+  const double err[3] = {tx - p1x, ty - p1y, ta - p1a};
+  const double gains[3] = {kp, kp / 5, kp / 2};
+  const double tb[3] = {0.1, 0.1, 0.1 * 10};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    double q = err[i] / (v1[i] + 0.01);
+    if (q < 0) q = -q;
+    const double nb = (q < tb[i]) ? 1.0 : 0.0;
+    const double x = err[i] * gains[i] - (v1[i] * nb) * kd;
+    act[i] = (float)(x < -1.0 ? -1.0 : (x > 1.0 ? 1.0 : x));
+  }
+  act[3] = (float)shoot_;
+}
+
+#undef SC
+}  // namespace hk

@@ -94,9 +94,10 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   if (const char *ab = std::getenv("HK_ABLATE")) c->cfg.ablate = std::atoi(ab);  // timing experiments only
   c->s.n = n;
   const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NIF * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
+  const size_t nw = (size_t)hk::workspace_words_per_arena() * n;
   if ((e = hipMalloc(&c->s.f, nf * 4)) != hipSuccess || (e = hipMalloc(&c->s.i, ni * 4)) != hipSuccess ||
       (e = hipMalloc(&c->s.man, nm * 4)) != hipSuccess || (e = hipMalloc(&c->s.phase, 2 * n * 8)) != hipSuccess ||
-      (e = hipMalloc(&c->s.counters, HK_NUM_COUNTERS * 8)) != hipSuccess) {
+      (e = hipMalloc(&c->s.ws, nw * 4)) != hipSuccess || (e = hipMalloc(&c->s.counters, HK_NUM_COUNTERS * 8)) != hipSuccess) {
     hk_destroy(c);
     return hipfail(e, "hk_create: hipMalloc");
   }
@@ -135,6 +136,7 @@ int hk_destroy(void *ctx) {
   if (c->s.f) (void)hipFree(c->s.f);
   if (c->s.i) (void)hipFree(c->s.i);
   if (c->s.man) (void)hipFree(c->s.man);
+  if (c->s.ws) (void)hipFree(c->s.ws);
   if (c->s.phase) (void)hipFree(c->s.phase);
   if (c->s.counters) (void)hipFree(c->s.counters);
   delete c;

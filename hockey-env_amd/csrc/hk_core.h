@@ -13,7 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef HK_DEV
 #define HK_DEV __device__ __forceinline__
+#endif
 
 namespace hk {
 
@@ -62,7 +64,7 @@ struct Scene {
   float friction[NP], restitution[NP];
   int manslot[NP];                                             // manifold slot or -1 (sensor)
   int edges[3][10];                                            // contact edges of each dynamic body
-  // broad-phase rejection data (performance only; results unchanged, see hk_world.h pair_far_*)
+  // broad-phase rejection data (performance only; results unchanged, see hk_arena.h pair_far_*)
   float fx_aabb[NF][4];   // world AABB of every static fixture {minx, miny, maxx, maxy}
   float rcore[3];         // max distance from a dynamic body's COM to its core (radius-free) shape
 };

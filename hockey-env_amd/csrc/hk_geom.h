@@ -1,0 +1,507 @@
+// hk_geom.h -- Box2D 2.3 geometry for the hockey scene: narrow phase (b2CollidePolygonAndCircle,
+// b2CollidePolygons, b2ClipSegmentToLine), GJK distance (b2Distance / b2TestOverlap), sweeps and
+// conservative-advancement time of impact (b2TimeOfImpact, b2SeparationFunction).
+// All functions are register-resident: fixtures come from __constant__ memory, simplex vertices are
+// named (no runtime-indexed private arrays), so nothing here touches scratch memory.
+// Float operation order matches the CPU test oracle bit for bit.
+#pragma once
+#include "hk_core.h"
+
+namespace hk {
+
+struct Manifold {
+  v2 pt_lp[2];
+  float ni[2], ti[2];
+  uint32_t id[2];
+  v2 ln, lp;
+  int type, count;  // type 1 = faceA, 2 = faceB
+};
+
+// ------------------------------------------------------------------------------------------------
+#define FXV(f, i) V((f).vx[i], (f).vy[i])
+#define FXN(f, i) V((f).nx[i], (f).ny[i])
+
+HK_DEV void collide_poly_circle(Manifold &m, const Fixture &pa, xform xfA, const Fixture &cb, xform xfB) {
+  m.count = 0;
+  v2 c = mul_xv(xfB, FXV(cb, 0));
+  v2 cl = mulT_xv(xfA, c);
+  int ni = 0;
+  float sep = -kFltMax;
+  float radius = pa.radius + cb.radius;
+  for (int i = 0; i < pa.count; ++i) {
+    float s = dot(FXN(pa, i), vsub(cl, FXV(pa, i)));
+    if (s > radius) return;
+    if (s > sep) { sep = s; ni = i; }
+  }
+  int i1 = ni, i2 = i1 + 1 < pa.count ? i1 + 1 : 0;
+  v2 v1 = FXV(pa, i1), v2_ = FXV(pa, i2);
+  if (sep < kFltEps) {
+    m.count = 1; m.type = 1; m.ln = FXN(pa, ni); m.lp = vs(0.5f, vadd(v1, v2_));
+    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+    return;
+  }
+  float u1 = dot(vsub(cl, v1), vsub(v2_, v1));
+  float u2 = dot(vsub(cl, v2_), vsub(v1, v2_));
+  if (u1 <= 0.0f) {
+    if (vdist2(cl, v1) > radius * radius) return;
+    m.count = 1; m.type = 1; m.ln = vsub(cl, v1); vnormalize(m.ln); m.lp = v1;
+    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+  } else if (u2 <= 0.0f) {
+    if (vdist2(cl, v2_) > radius * radius) return;
+    m.count = 1; m.type = 1; m.ln = vsub(cl, v2_); vnormalize(m.ln); m.lp = v2_;
+    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+  } else {
+    v2 fc = vs(0.5f, vadd(v1, v2_));
+    float s = dot(vsub(cl, fc), FXN(pa, i1));
+    if (s > radius) return;
+    m.count = 1; m.type = 1; m.ln = FXN(pa, i1); m.lp = fc;
+    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+  }
+}
+
+HK_DEV float find_max_separation(int &edge, const Fixture &p1, xform xf1, const Fixture &p2, xform xf2) {
+  xform xf = mulT_xx(xf2, xf1);
+  int best = 0;
+  float maxs = -kFltMax;
+  for (int i = 0; i < p1.count; ++i) {
+    v2 n = mul_rv(xf.q, FXN(p1, i));
+    v2 v1 = mul_xv(xf, FXV(p1, i));
+    float si = kFltMax;
+    for (int j = 0; j < p2.count; ++j) {
+      float sij = dot(n, vsub(FXV(p2, j), v1));
+      if (sij < si) si = sij;
+    }
+    if (si > maxs) { maxs = si; best = i; }
+  }
+  edge = best;
+  return maxs;
+}
+
+struct ClipV { v2 v; uint32_t id; };
+HK_DEV uint32_t cf_id(uint32_t ia, uint32_t ib, uint32_t ta, uint32_t tb) { return ia | (ib << 8) | (ta << 16) | (tb << 24); }
+
+HK_DEV void find_incident_edge(ClipV c[2], const Fixture &p1, xform xf1, int edge1, const Fixture &p2, xform xf2) {
+  v2 n1 = mulT_rv(xf2.q, mul_rv(xf1.q, FXN(p1, edge1)));
+  int index = 0;
+  float mind = kFltMax;
+  for (int i = 0; i < p2.count; ++i) {
+    float d = dot(n1, FXN(p2, i));
+    if (d < mind) { mind = d; index = i; }
+  }
+  int i1 = index, i2 = i1 + 1 < p2.count ? i1 + 1 : 0;
+  c[0].v = mul_xv(xf2, FXV(p2, i1));
+  c[0].id = cf_id(edge1, i1, 1, 0);
+  c[1].v = mul_xv(xf2, FXV(p2, i2));
+  c[1].id = cf_id(edge1, i2, 1, 0);
+}
+
+HK_DEV int clip_segment(ClipV out[2], const ClipV in[2], v2 normal, float offset, int vA) {
+  int n = 0;
+  float d0 = dot(normal, in[0].v) - offset;
+  float d1 = dot(normal, in[1].v) - offset;
+  if (d0 <= 0.0f) out[n++] = in[0];
+  if (d1 <= 0.0f) out[n++] = in[1];
+  if (d0 * d1 < 0.0f) {
+    float interp = d0 / (d0 - d1);
+    out[n].v = vadd(in[0].v, vs(interp, vsub(in[1].v, in[0].v)));
+    out[n].id = cf_id(vA, (in[0].id >> 8) & 0xffu, 0, 1);
+    ++n;
+  }
+  return n;
+}
+
+HK_DEV void collide_polygons(Manifold &m, const Fixture &pA, xform xfA, const Fixture &pB, xform xfB) {
+  m.count = 0;
+  float total = pA.radius + pB.radius;
+  int eA = 0, eB = 0;
+  float sA = find_max_separation(eA, pA, xfA, pB, xfB);
+  if (sA > total) return;
+  float sB = find_max_separation(eB, pB, xfB, pA, xfA);
+  if (sB > total) return;
+  const float k_tol = 0.1f * kLinearSlop;
+  const bool flip = sB > sA + k_tol;
+  const Fixture &p1 = flip ? pB : pA;
+  const Fixture &p2 = flip ? pA : pB;
+  xform xf1 = flip ? xfB : xfA, xf2 = flip ? xfA : xfB;
+  int edge1 = flip ? eB : eA;
+  m.type = flip ? 2 : 1;
+  ClipV inc[2];
+  find_incident_edge(inc, p1, xf1, edge1, p2, xf2);
+  int iv1 = edge1, iv2 = edge1 + 1 < p1.count ? edge1 + 1 : 0;
+  v2 v11 = FXV(p1, iv1), v12 = FXV(p1, iv2);
+  v2 lt = vsub(v12, v11);
+  vnormalize(lt);
+  v2 ln = crs_vs(lt, 1.0f);
+  v2 pp = vs(0.5f, vadd(v11, v12));
+  v2 tangent = mul_rv(xf1.q, lt);
+  v2 normal = crs_vs(tangent, 1.0f);
+  v11 = mul_xv(xf1, v11);
+  v12 = mul_xv(xf1, v12);
+  float front = dot(normal, v11);
+  float side1 = -dot(tangent, v11) + total;
+  float side2 = dot(tangent, v12) + total;
+  ClipV cp1[2], cp2[2];
+  int np = clip_segment(cp1, inc, vneg(tangent), side1, iv1);
+  if (np < 2) return;
+  np = clip_segment(cp2, cp1, tangent, side2, iv2);
+  if (np < 2) return;
+  m.ln = ln;
+  m.lp = pp;
+  int pc = 0;
+  for (int i = 0; i < 2; ++i) {
+    float sep = dot(normal, cp2[i].v) - front;
+    if (sep <= total) {
+      m.pt_lp[pc] = mulT_xv(xf2, cp2[i].v);
+      uint32_t id = cp2[i].id;
+      if (flip) id = cf_id((id >> 8) & 0xffu, id & 0xffu, (id >> 24) & 0xffu, (id >> 16) & 0xffu);
+      m.id[pc] = id;
+      ++pc;
+    }
+  }
+  m.count = pc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// GJK distance + TOI (b2Distance.cpp, b2TimeOfImpact.cpp)
+// ------------------------------------------------------------------------------------------------
+struct Proxy { const float *vx, *vy; int count; float radius; };
+HK_DEV Proxy make_proxy(const Fixture &f) { Proxy p; p.vx = f.vx; p.vy = f.vy; p.count = f.count; p.radius = f.radius; return p; }
+HK_DEV v2 pv(const Proxy &p, int i) { return V(p.vx[i], p.vy[i]); }
+HK_DEV int proxy_support(const Proxy &p, v2 d) {
+  int best = 0;
+  float bv = dot(pv(p, 0), d);
+  for (int i = 1; i < p.count; ++i) {
+    float v = dot(pv(p, i), d);
+    if (v > bv) { best = i; bv = v; }
+  }
+  return best;
+}
+
+// ---- GJK with a register-resident simplex (b2Simplex m_v1/m_v2/m_v3) ----
+struct SimplexCache { float metric; int count; int iA[3], iB[3]; };
+struct SVert { v2 wA, wB, w; float a; int iA, iB; };
+struct Simplex { SVert v1, v2, v3; int count; };
+
+HK_DEV float simplex_metric(const Simplex &s) {
+  if (s.count == 2) return vdist(s.v1.w, s.v2.w);
+  if (s.count == 3) return crs(vsub(s.v2.w, s.v1.w), vsub(s.v3.w, s.v1.w));
+  return 0.0f;
+}
+HK_DEV SVert make_svert(const Proxy &pA, xform xA, const Proxy &pB, xform xB, int iA, int iB) {
+  SVert v;
+  v.iA = iA;
+  v.iB = iB;
+  v.wA = mul_xv(xA, pv(pA, iA));
+  v.wB = mul_xv(xB, pv(pB, iB));
+  v.w = vsub(v.wB, v.wA);
+  v.a = 0.0f;
+  return v;
+}
+HK_DEV void simplex_read(Simplex &s, const SimplexCache &cache, const Proxy &pA, xform xA, const Proxy &pB, xform xB) {
+  s.count = cache.count;
+  s.v1.wA = s.v1.wB = s.v1.w = V(0.0f, 0.0f);
+  s.v1.a = 0.0f;
+  s.v1.iA = s.v1.iB = 0;
+  s.v2 = s.v1;
+  s.v3 = s.v1;
+  if (s.count > 0) s.v1 = make_svert(pA, xA, pB, xB, cache.iA[0], cache.iB[0]);
+  if (s.count > 1) s.v2 = make_svert(pA, xA, pB, xB, cache.iA[1], cache.iB[1]);
+  if (s.count > 2) s.v3 = make_svert(pA, xA, pB, xB, cache.iA[2], cache.iB[2]);
+  if (s.count > 1) {
+    float m1 = cache.metric, m2 = simplex_metric(s);
+    if (m2 < 0.5f * m1 || 2.0f * m1 < m2 || m2 < kFltEps) s.count = 0;
+  }
+  if (s.count == 0) {
+    s.v1 = make_svert(pA, xA, pB, xB, 0, 0);
+    s.v1.a = 1.0f;
+    s.count = 1;
+  }
+}
+HK_DEV void simplex_write(const Simplex &s, SimplexCache &cache) {
+  cache.metric = simplex_metric(s);
+  cache.count = s.count;
+  cache.iA[0] = s.v1.iA; cache.iB[0] = s.v1.iB;
+  cache.iA[1] = s.v2.iA; cache.iB[1] = s.v2.iB;
+  cache.iA[2] = s.v3.iA; cache.iB[2] = s.v3.iB;
+}
+HK_DEV v2 simplex_search_dir(const Simplex &s) {
+  if (s.count == 1) return vneg(s.v1.w);
+  v2 e12 = vsub(s.v2.w, s.v1.w);
+  float sgn = crs(e12, vneg(s.v1.w));
+  if (sgn > 0.0f) return crs_sv(1.0f, e12);
+  return crs_vs(e12, 1.0f);
+}
+HK_DEV void simplex_witness(const Simplex &s, v2 &pA, v2 &pB) {
+  if (s.count == 1) { pA = s.v1.wA; pB = s.v1.wB; }
+  else if (s.count == 2) {
+    pA = vadd(vs(s.v1.a, s.v1.wA), vs(s.v2.a, s.v2.wA));
+    pB = vadd(vs(s.v1.a, s.v1.wB), vs(s.v2.a, s.v2.wB));
+  } else {
+    pA = vadd(vadd(vs(s.v1.a, s.v1.wA), vs(s.v2.a, s.v2.wA)), vs(s.v3.a, s.v3.wA));
+    pB = pA;
+  }
+}
+HK_DEV void solve2(Simplex &s) {
+  v2 w1 = s.v1.w, w2 = s.v2.w;
+  v2 e12 = vsub(w2, w1);
+  float d12_2 = -dot(w1, e12);
+  if (d12_2 <= 0.0f) { s.v1.a = 1.0f; s.count = 1; return; }
+  float d12_1 = dot(w2, e12);
+  if (d12_1 <= 0.0f) { s.v2.a = 1.0f; s.count = 1; s.v1 = s.v2; return; }
+  float inv = 1.0f / (d12_1 + d12_2);
+  s.v1.a = d12_1 * inv;
+  s.v2.a = d12_2 * inv;
+  s.count = 2;
+}
+HK_DEV void solve3(Simplex &s) {
+  v2 w1 = s.v1.w, w2 = s.v2.w, w3 = s.v3.w;
+  v2 e12 = vsub(w2, w1);
+  float w1e12 = dot(w1, e12), w2e12 = dot(w2, e12);
+  float d12_1 = w2e12, d12_2 = -w1e12;
+  v2 e13 = vsub(w3, w1);
+  float w1e13 = dot(w1, e13), w3e13 = dot(w3, e13);
+  float d13_1 = w3e13, d13_2 = -w1e13;
+  v2 e23 = vsub(w3, w2);
+  float w2e23 = dot(w2, e23), w3e23 = dot(w3, e23);
+  float d23_1 = w3e23, d23_2 = -w2e23;
+  float n123 = crs(e12, e13);
+  float d123_1 = n123 * crs(w2, w3);
+  float d123_2 = n123 * crs(w3, w1);
+  float d123_3 = n123 * crs(w1, w2);
+  if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v1.a = 1.0f; s.count = 1; return; }
+  if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) {
+    float inv = 1.0f / (d12_1 + d12_2);
+    s.v1.a = d12_1 * inv; s.v2.a = d12_2 * inv; s.count = 2; return;
+  }
+  if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) {
+    float inv = 1.0f / (d13_1 + d13_2);
+    s.v1.a = d13_1 * inv; s.v3.a = d13_2 * inv; s.count = 2; s.v2 = s.v3; return;
+  }
+  if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v2.a = 1.0f; s.count = 1; s.v1 = s.v2; return; }
+  if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v3.a = 1.0f; s.count = 1; s.v1 = s.v3; return; }
+  if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) {
+    float inv = 1.0f / (d23_1 + d23_2);
+    s.v2.a = d23_1 * inv; s.v3.a = d23_2 * inv; s.count = 2; s.v1 = s.v3; return;
+  }
+  float inv = 1.0f / (d123_1 + d123_2 + d123_3);
+  s.v1.a = d123_1 * inv; s.v2.a = d123_2 * inv; s.v3.a = d123_3 * inv; s.count = 3;
+}
+
+// b2Distance (returns the distance; witness points are not needed by the callers)
+HK_DEV float gjk_distance(SimplexCache &cache, const Proxy &pA, xform xA, const Proxy &pB, xform xB, int use_radii) {
+  Simplex s;
+  simplex_read(s, cache, pA, xA, pB, xB);
+  int sA0 = 0, sA1 = 0, sA2 = 0, sB0 = 0, sB1 = 0, sB2 = 0, saveCount;
+  int iter = 0;
+  while (iter < 20) {
+    saveCount = s.count;
+    sA0 = s.v1.iA; sB0 = s.v1.iB;
+    sA1 = s.v2.iA; sB1 = s.v2.iB;
+    sA2 = s.v3.iA; sB2 = s.v3.iB;
+    if (s.count == 2) solve2(s);
+    else if (s.count == 3) solve3(s);
+    if (s.count == 3) break;
+    v2 d = simplex_search_dir(s);
+    if (vlen2(d) < kFltEps * kFltEps) break;
+    const int iA = proxy_support(pA, mulT_rv(xA.q, vneg(d)));
+    const int iB = proxy_support(pB, mulT_rv(xB.q, d));
+    SVert nv;
+    nv.iA = iA;
+    nv.wA = mul_xv(xA, pv(pA, iA));
+    nv.iB = iB;
+    nv.wB = mul_xv(xB, pv(pB, iB));
+    nv.w = vsub(nv.wB, nv.wA);
+    nv.a = 0.0f;
+    if (s.count == 1) s.v2 = nv; else s.v3 = nv;
+    ++iter;
+    bool dup = (saveCount > 0 && iA == sA0 && iB == sB0) || (saveCount > 1 && iA == sA1 && iB == sB1) ||
+               (saveCount > 2 && iA == sA2 && iB == sB2);
+    if (dup) break;
+    ++s.count;
+  }
+  v2 pa, pb;
+  simplex_witness(s, pa, pb);
+  float dist = vdist(pa, pb);
+  simplex_write(s, cache);
+  if (use_radii) {
+    float rA = pA.radius, rB = pB.radius;
+    if (dist > rA + rB && dist > kFltEps) dist -= rA + rB;
+    else dist = 0.0f;
+  }
+  return dist;
+}
+
+HK_DEV int test_overlap(const Fixture &fA, xform xA, const Fixture &fB, xform xB) {
+  Proxy pA = make_proxy(fA), pB = make_proxy(fB);
+  SimplexCache cache;
+  cache.count = 0;
+  cache.metric = 0.0f;
+  float d = gjk_distance(cache, pA, xA, pB, xB, 1);
+  return d < 10.0f * kFltEps;
+}
+
+struct Sweep { v2 lc, c0, c; float a0, a, alpha0; };
+HK_DEV void sweep_xf(const Sweep &s, xform &xf, float beta) {
+  xf.p = vadd(vs(1.0f - beta, s.c0), vs(beta, s.c));
+  float angle = (1.0f - beta) * s.a0 + beta * s.a;
+  xf.q = rot_set(angle);
+  xf.p = vsub(xf.p, mul_rv(xf.q, s.lc));
+}
+HK_DEV void sweep_advance(Sweep &s, float alpha) {
+  float beta = (alpha - s.alpha0) / (1.0f - s.alpha0);
+  s.c0 = vadd(s.c0, vs(beta, vsub(s.c, s.c0)));
+  s.a0 += beta * (s.a - s.a0);
+  s.alpha0 = alpha;
+}
+HK_DEV void sweep_normalize(Sweep &s) {
+  float twoPi = 2.0f * kPi;
+  float d = twoPi * floorf(s.a0 / twoPi);
+  s.a0 -= d;
+  s.a -= d;
+}
+
+enum { SF_POINTS = 0, SF_FACEA, SF_FACEB };
+struct SepFn { Proxy pA, pB; Sweep sA, sB; int type; v2 lp, axis; };
+
+HK_DEV void sep_init(SepFn &f, const SimplexCache &cache, const Proxy &pA, const Sweep &sA, const Proxy &pB,
+                     const Sweep &sB, float t1) {
+  f.pA = pA; f.pB = pB; f.sA = sA; f.sB = sB;
+  xform xA, xB;
+  sweep_xf(f.sA, xA, t1);
+  sweep_xf(f.sB, xB, t1);
+  if (cache.count == 1) {
+    f.type = SF_POINTS;
+    v2 a = mul_xv(xA, pv(pA, cache.iA[0]));
+    v2 b = mul_xv(xB, pv(pB, cache.iB[0]));
+    f.axis = vsub(b, a);
+    vnormalize(f.axis);
+  } else if (cache.iA[0] == cache.iA[1]) {
+    f.type = SF_FACEB;
+    v2 b1 = pv(pB, cache.iB[0]), b2 = pv(pB, cache.iB[1]);
+    f.axis = crs_vs(vsub(b2, b1), 1.0f);
+    vnormalize(f.axis);
+    v2 normal = mul_rv(xB.q, f.axis);
+    f.lp = vs(0.5f, vadd(b1, b2));
+    v2 pb = mul_xv(xB, f.lp);
+    v2 pa = mul_xv(xA, pv(pA, cache.iA[0]));
+    float s = dot(vsub(pa, pb), normal);
+    if (s < 0.0f) f.axis = vneg(f.axis);
+  } else {
+    f.type = SF_FACEA;
+    v2 a1 = pv(pA, cache.iA[0]), a2 = pv(pA, cache.iA[1]);
+    f.axis = crs_vs(vsub(a2, a1), 1.0f);
+    vnormalize(f.axis);
+    v2 normal = mul_rv(xA.q, f.axis);
+    f.lp = vs(0.5f, vadd(a1, a2));
+    v2 pa = mul_xv(xA, f.lp);
+    v2 pb = mul_xv(xB, pv(pB, cache.iB[0]));
+    float s = dot(vsub(pb, pa), normal);
+    if (s < 0.0f) f.axis = vneg(f.axis);
+  }
+}
+HK_DEV float sep_find_min(const SepFn &f, int &iA, int &iB, float t) {
+  xform xA, xB;
+  sweep_xf(f.sA, xA, t);
+  sweep_xf(f.sB, xB, t);
+  if (f.type == SF_POINTS) {
+    v2 axA = mulT_rv(xA.q, f.axis), axB = mulT_rv(xB.q, vneg(f.axis));
+    iA = proxy_support(f.pA, axA);
+    iB = proxy_support(f.pB, axB);
+    v2 a = mul_xv(xA, pv(f.pA, iA)), b = mul_xv(xB, pv(f.pB, iB));
+    return dot(vsub(b, a), f.axis);
+  } else if (f.type == SF_FACEA) {
+    v2 normal = mul_rv(xA.q, f.axis);
+    v2 a = mul_xv(xA, f.lp);
+    v2 axB = mulT_rv(xB.q, vneg(normal));
+    iA = -1;
+    iB = proxy_support(f.pB, axB);
+    v2 b = mul_xv(xB, pv(f.pB, iB));
+    return dot(vsub(b, a), normal);
+  } else {
+    v2 normal = mul_rv(xB.q, f.axis);
+    v2 b = mul_xv(xB, f.lp);
+    v2 axA = mulT_rv(xA.q, vneg(normal));
+    iB = -1;
+    iA = proxy_support(f.pA, axA);
+    v2 a = mul_xv(xA, pv(f.pA, iA));
+    return dot(vsub(a, b), normal);
+  }
+}
+HK_DEV float sep_eval(const SepFn &f, int iA, int iB, float t) {
+  xform xA, xB;
+  sweep_xf(f.sA, xA, t);
+  sweep_xf(f.sB, xB, t);
+  if (f.type == SF_POINTS) {
+    v2 a = mul_xv(xA, pv(f.pA, iA)), b = mul_xv(xB, pv(f.pB, iB));
+    return dot(vsub(b, a), f.axis);
+  } else if (f.type == SF_FACEA) {
+    v2 normal = mul_rv(xA.q, f.axis);
+    v2 a = mul_xv(xA, f.lp);
+    v2 b = mul_xv(xB, pv(f.pB, iB));
+    return dot(vsub(b, a), normal);
+  } else {
+    v2 normal = mul_rv(xB.q, f.axis);
+    v2 b = mul_xv(xB, f.lp);
+    v2 a = mul_xv(xA, pv(f.pA, iA));
+    return dot(vsub(a, b), normal);
+  }
+}
+
+enum { TOI_UNKNOWN = 0, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
+
+HK_DEV int time_of_impact(const Proxy &pA, const Proxy &pB, Sweep sA, Sweep sB, float tMax, float &t_out) {
+  int state = TOI_UNKNOWN;
+  t_out = tMax;
+  sweep_normalize(sA);
+  sweep_normalize(sB);
+  float total = pA.radius + pB.radius;
+  float target = fmax2(kLinearSlop, total - 3.0f * kLinearSlop);
+  float tol = 0.25f * kLinearSlop;
+  float t1 = 0.0f;
+  int iter = 0;
+  SimplexCache cache;
+  cache.count = 0;
+  cache.metric = 0.0f;
+  for (;;) {
+    xform xA, xB;
+    sweep_xf(sA, xA, t1);
+    sweep_xf(sB, xB, t1);
+    float dist = gjk_distance(cache, pA, xA, pB, xB, 0);
+    if (dist <= 0.0f) { state = TOI_OVERLAPPED; t_out = 0.0f; break; }
+    if (dist < target + tol) { state = TOI_TOUCHING; t_out = t1; break; }
+    SepFn fcn;
+    sep_init(fcn, cache, pA, sA, pB, sB, t1);
+    int done = 0;
+    float t2 = tMax;
+    int push = 0;
+    for (;;) {
+      int iA, iB;
+      float s2 = sep_find_min(fcn, iA, iB, t2);
+      if (s2 > target + tol) { state = TOI_SEPARATED; t_out = tMax; done = 1; break; }
+      if (s2 > target - tol) { t1 = t2; break; }
+      float s1 = sep_eval(fcn, iA, iB, t1);
+      if (s1 < target - tol) { state = TOI_FAILED; t_out = t1; done = 1; break; }
+      if (s1 <= target + tol) { state = TOI_TOUCHING; t_out = t1; done = 1; break; }
+      int rit = 0;
+      float a1 = t1, a2 = t2;
+      for (;;) {
+        float t;
+        if (rit & 1) t = a1 + (target - s1) * (a2 - a1) / (s2 - s1);
+        else t = 0.5f * (a1 + a2);
+        ++rit;
+        float s = sep_eval(fcn, iA, iB, t);
+        if (fabs2(s - target) < tol) { t2 = t; break; }
+        if (s > target) { a1 = t; s1 = s; } else { a2 = t; s2 = s; }
+        if (rit == 50) break;
+      }
+      ++push;
+      if (push == kMaxPolyVerts) break;
+    }
+    ++iter;
+    if (done) break;
+    if (iter == 20) { state = TOI_FAILED; t_out = t1; break; }
+  }
+  return state;
+}
+
+}  // namespace hk

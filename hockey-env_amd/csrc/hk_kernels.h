@@ -20,6 +20,7 @@ struct DevState {
   float *f;
   int32_t *i;
   float *man;
+  float *ws;  // large-island slot workspace [kBigC][kSlotWords][N] (hk_solver.h HbmSlots)
   double *phase;
   unsigned long long *counters;
   int64_t n;
@@ -30,7 +31,7 @@ struct KCfg {
   int policy[2];
   uint64_t seed;
   int64_t arena_offset;
-  int ablate;  // timing-only ablations (bit0 vel iters, bit1 pos iters, bit2 TOI, bit3 collide); 0 in product
+  int ablate;  // diagnostics only (HK_ABLATE env): bit0 forces the generic large-island solver; 0 in product
 };
 
 struct StepIO {
@@ -51,6 +52,7 @@ hipError_t launch_get_state(const DevState &s, const KCfg &cfg, float *state, in
 hipError_t launch_set_state(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *state,
                             const int32_t *aux, hipStream_t st);
 hipError_t upload_scene(const Scene &sc);
+int64_t workspace_words_per_arena();
 
 // host-side scene construction (hk_scene.cpp): Box2D 2.3 hull / normals / mass data of hockey_env.py's
 // fixtures, and the canonical contact pair table.

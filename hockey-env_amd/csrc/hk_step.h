@@ -1,0 +1,424 @@
+// hk_step.h -- per-arena entry points of the hot path: HBM state <-> register arena, HockeyEnv.reset,
+// HockeyEnv.step (one lane = one arena).  The __global__ wrappers live in hk_kernels.hip.
+//
+// HBM layout (struct of arrays, arena index innermost so a wave's 64 lanes touch 64 consecutive dwords
+// of every field):
+//   f[NFF][N]            float  body state: per dynamic body {origin x,y, COM x,y, angle, vx, vy, w,
+//                               sleep time} + the puck's pending force (TRAIN_DEFENSE reset)
+//   i[NIF][N]            int32  awake bits, has_puck1/2, time, done, winner, max_t, touching mask,
+//                               enabled mask, one_starts, episode and step counters
+//   man[NSOLID][NMF][N]  float  Box2D manifold of every solid pair (read/written in place, touching only)
+//   phase[2][N]          double BasicOpponent phases (global np.random stream -> per-arena Philox)
+#pragma once
+#include "hk_arena.h"
+
+namespace hk {
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based RNG): key = seed, counter = (arena lo, arena hi, step/episode, purpose)
+// ------------------------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+HK_DEV U4 philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  U4 c = {c0, c1, c2, c3};
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    U4 n = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+HK_DEV float u01f(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+HK_DEV double u01d(uint32_t a, uint32_t b) {  // numpy random_double construction (53 bits)
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
+enum { RNG_ACTION = 1, RNG_PHASE = 2, RNG_RESET = 3, RNG_PHASE0 = 4 };
+
+// ------------------------------------------------------------------------------------------------
+// world <-> HBM
+// ------------------------------------------------------------------------------------------------
+HK_DEV float &F(const DevState &s, int field, int64_t a) { return s.f[(int64_t)field * s.n + a]; }
+HK_DEV int32_t &I(const DevState &s, int field, int64_t a) { return s.i[(int64_t)field * s.n + a]; }
+HK_DEV float &M(const DevState &s, int slot, int field, int64_t a) {
+  return s.man[((int64_t)slot * NMF + field) * s.n + a];
+}
+
+HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, int vel_ref, float *lds, int lane) {
+  const int awake = I(s, I_AWAKE, a);
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int o = b * FB;
+    w.d.px[b] = F(s, o + FB_PX, a);
+    w.d.py[b] = F(s, o + FB_PY, a);
+    w.d.cx[b] = F(s, o + FB_CX, a);
+    w.d.cy[b] = F(s, o + FB_CY, a);
+    w.d.a[b] = F(s, o + FB_A, a);
+    const rot q = rot_set(w.d.a[b]);
+    w.d.qs[b] = q.s;
+    w.d.qc[b] = q.c;
+    w.d.c0x[b] = w.d.cx[b];
+    w.d.c0y[b] = w.d.cy[b];
+    w.d.a0[b] = w.d.a[b];
+    w.d.al0[b] = 0.0f;
+    w.d.vx[b] = F(s, o + FB_VX, a);
+    w.d.vy[b] = F(s, o + FB_VY, a);
+    w.d.w[b] = F(s, o + FB_W, a);
+    w.d.sleep[b] = F(s, o + FB_SLEEP, a);
+    w.d.awake[b] = (awake >> b) & 1;
+    w.d.fx[b] = 0.0f;
+    w.d.fy[b] = 0.0f;
+    w.d.tq[b] = 0.0f;
+    w.d.ld[b] = 0.0f;
+    w.d.ad[b] = 0.0f;
+  }
+  w.d.fx[B_PK] = F(s, F_PFX, a);
+  w.d.fy[B_PK] = F(s, F_PFY, a);
+  w.keep_mode = keep_mode;
+  w.vel_ref = vel_ref;
+  w.has1 = I(s, I_HAS1, a);
+  w.has2 = I(s, I_HAS2, a);
+  w.time = I(s, I_TIME, a);
+  w.done = I(s, I_DONE, a);
+  w.winner = I(s, I_WINNER, a);
+  w.max_t = I(s, I_MAXT, a);
+  w.n_toi = 0;
+  w.overflow = 0;
+  w.n_big = 0;
+  w.force_big = 0;
+  w.touch = (uint32_t)I(s, I_TOUCH, a);
+  w.enabled = (uint32_t)I(s, I_ENABLED, a);
+  w.toiflag = w.cisl = w.bisl = 0u;
+  w.man = s.man;
+  w.ws = s.ws;
+  w.n = s.n;
+  w.a = a;
+  w.lds = lds;
+  w.lane = lane;
+#ifdef HK_TRACE
+  w.trace = nullptr;
+#endif
+}
+
+HK_DEV void store_arena(const Arena &w, const DevState &s, int64_t a) {
+  int awake = 0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int o = b * FB;
+    F(s, o + FB_PX, a) = w.d.px[b];
+    F(s, o + FB_PY, a) = w.d.py[b];
+    F(s, o + FB_CX, a) = w.d.cx[b];
+    F(s, o + FB_CY, a) = w.d.cy[b];
+    F(s, o + FB_A, a) = w.d.a[b];
+    F(s, o + FB_VX, a) = w.d.vx[b];
+    F(s, o + FB_VY, a) = w.d.vy[b];
+    F(s, o + FB_W, a) = w.d.w[b];
+    F(s, o + FB_SLEEP, a) = w.d.sleep[b];
+    awake |= (w.d.awake[b] & 1) << b;
+  }
+  F(s, F_PFX, a) = w.d.fx[B_PK];
+  F(s, F_PFY, a) = w.d.fy[B_PK];
+  I(s, I_AWAKE, a) = awake;
+  I(s, I_HAS1, a) = w.has1;
+  I(s, I_HAS2, a) = w.has2;
+  I(s, I_TIME, a) = w.time;
+  I(s, I_DONE, a) = w.done;
+  I(s, I_WINNER, a) = w.winner;
+  I(s, I_MAXT, a) = w.max_t;
+  I(s, I_TOUCH, a) = (int)w.touch;
+  I(s, I_ENABLED, a) = (int)w.enabled;
+}
+
+// HockeyEnv.reset body re-creation (hockey_env.py:345-418) from placement params.
+// player*_has_puck is NOT cleared (the reference's reset never assigns it).
+HK_DEV void reset_arena(Arena &w, const float *p6, int max_t) {
+  const float ix[3] = {2.0f, p6[0], p6[2]}, iy[3] = {4.0f, p6[1], p6[3]};
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const rot q = rot_set(0.0f);
+    xform x;
+    x.p = V(ix[b], iy[b]);
+    x.q = q;
+    const v2 c = mul_xv(x, V(g_scene.lcx[b], g_scene.lcy[b]));
+    w.d.px[b] = ix[b];
+    w.d.py[b] = iy[b];
+    w.d.qs[b] = q.s;
+    w.d.qc[b] = q.c;
+    w.d.a[b] = w.d.a0[b] = 0.0f;
+    w.d.al0[b] = 0.0f;
+    w.d.cx[b] = w.d.c0x[b] = c.x;
+    w.d.cy[b] = w.d.c0y[b] = c.y;
+    w.d.vx[b] = w.d.vy[b] = w.d.w[b] = 0.0f;
+    w.d.fx[b] = w.d.fy[b] = w.d.tq[b] = 0.0f;
+    w.d.ld[b] = w.d.ad[b] = 0.0f;
+    w.d.sleep[b] = 0.0f;
+    w.d.awake[b] = 1;
+  }
+  w.d.ld[B_PK] = 0.05f;
+  if (p6[4] != 0.0f || p6[5] != 0.0f) apply_force<B_PK>(w, V(p6[4], p6[5]));
+  w.touch = 0u;
+  w.enabled = (1u << NP) - 1u;
+  w.max_t = max_t;
+  w.time = 0;
+  w.done = 0;
+  w.winner = 0;
+}
+
+// device placement (same formulas as hockey_amd/placement.py with Philox uniforms instead of PCG64)
+HK_DEV void device_placement(uint64_t seed, int64_t a, uint32_t episode, int mode, int one_starts, float *p6,
+                             int &max_t) {
+  const double W = 10.0, H = 8.0;
+  U4 r0 = philox(seed, (uint32_t)a, (uint32_t)(a >> 32), episode, RNG_RESET);
+  U4 r1 = philox(seed, (uint32_t)a, (uint32_t)(a >> 32), episode, RNG_RESET + 0x100);
+  double u[4] = {u01d(r0.x, r0.y), u01d(r0.z, r0.w), u01d(r1.x, r1.y), u01d(r1.z, r1.w)};
+  U4 r2 = philox(seed, (uint32_t)a, (uint32_t)(a >> 32), episode, RNG_RESET + 0x200);
+  double u4 = u01d(r2.x, r2.y);
+  int k = 0;
+  auto unif = [&](double lo, double hi) { double x = (k < 4) ? u[k] : u4; ++k; return lo + (hi - lo) * x; };
+  max_t = mode == 0 ? 250 : 80;
+  double p2x = 4 * W / 5, p2y = H / 2;
+  if (mode != 0) {
+    p2x = 4 * W / 5 + unif(-W / 3, W / 6);
+    p2y = H / 2 + unif(-H / 4, H / 4);
+  }
+  double px, py;
+  float fx = 0.0f, fy = 0.0f;
+  if (mode == 0 || mode == 1) {
+    if (one_starts || mode == 1) {
+      px = W / 2 - unif(H / 8, H / 4);
+      py = H / 2 + unif(-H / 8, H / 8);
+    } else {
+      px = W / 2 + unif(H / 8, H / 4);
+      py = H / 2 + unif(-H / 8, H / 8);
+    }
+  } else {
+    px = W / 2 + unif(0, W / 3);
+    py = H / 2 + 0.8 * unif(-H / 2, H / 2);
+    float aim = (float)(H / 2 + .6 * unif(-75.0 / 60.0, 75.0 / 60.0));
+    float dx = (float)px - 0.0f, dy = (float)py - aim;
+    float ln = sqrtf(dx * dx + dy * dy);
+    dx = dx / ln;
+    dy = dy / ln;
+    const float m = g_scene.mass[B_PK];
+    fx = ((-dx * 60.0f) * m) / 0.02f;
+    fy = ((-dy * 60.0f) * m) / 0.02f;
+  }
+  p6[0] = (float)p2x; p6[1] = (float)p2y; p6[2] = (float)px; p6[3] = (float)py; p6[4] = fx; p6[5] = fy;
+}
+
+HK_DEV void write_info(float *dst, int64_t a, const double *info) {
+  for (int k = 0; k < 4; ++k) dst[a * 4 + k] = (float)info[k];
+}
+
+// HockeyEnv.reset of arena a: explicit placement params or device placement (Philox), one_starting toggle.
+HK_DEV void reset_lane(const DevState &s, const KCfg &cfg, int64_t a, const float *params, const int32_t *max_t_in,
+                       const uint8_t *one_in) {
+  Arena w;
+  load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, nullptr, 0);
+  float p6[6];
+  int mt;
+  int one = I(s, I_ONE, a);
+  if (params) {
+    for (int k = 0; k < 6; ++k) p6[k] = params[a * 6 + k];
+    mt = cfg.mode == 0 ? 250 : 80;
+    if (cfg.mode == 0) one = one_in ? (int)one_in[a] : !one;
+  } else {
+    if (cfg.mode == 0) one = one_in ? (int)one_in[a] : !one;
+    const uint32_t ep = (uint32_t)I(s, I_EPISODE, a);
+    device_placement(cfg.seed, cfg.arena_offset + a, ep, cfg.mode, one, p6, mt);
+  }
+  if (max_t_in) mt = max_t_in[a];
+  reset_arena(w, p6, mt);
+  store_arena(w, s, a);
+  I(s, I_ONE, a) = one;
+  I(s, I_EPISODE, a) = I(s, I_EPISODE, a) + 1;
+}
+
+// One HockeyEnv.step of arena a (auto-reset, policy actions, pre-solve laws, world.Step, outputs).
+struct LaneOut { int done_edge, win1, win2, ntoi, ovf, nbig; };
+
+HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int64_t a, float *lds, int lane,
+                      PhaseT &T, LaneOut &out) {
+  Arena w;
+  load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, lds, lane);
+  w.force_big = cfg.ablate & 1;
+#ifdef HK_TRACE
+  w.trace = io.debug ? io.debug + a * kTraceStride : nullptr;
+#endif
+  const uint32_t stepc = (uint32_t)I(s, I_STEP, a);
+  if (cfg.auto_reset && w.done) {
+    int one = I(s, I_ONE, a);
+    if (cfg.mode == 0) one = !one;
+    const uint32_t ep = (uint32_t)I(s, I_EPISODE, a);
+    float p6[6];
+    int mt;
+    device_placement(cfg.seed, cfg.arena_offset + a, ep, cfg.mode, one, p6, mt);
+    reset_arena(w, p6, mt);
+    I(s, I_ONE, a) = one;
+    I(s, I_EPISODE, a) = (int)(ep + 1);
+  }
+  // ---- actions: external / Philox random / fused BasicOpponent ----
+  float a8[8];
+  for (int p = 0; p < 2; ++p) {
+    const int pol = cfg.policy[p];
+    if (pol == 0) {
+      for (int k = 0; k < 4; ++k) a8[4 * p + k] = io.actions ? io.actions[a * 8 + 4 * p + k] : 0.0f;
+    } else if (pol == 1) {
+      const int64_t ga = cfg.arena_offset + a;
+      U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), stepc, RNG_ACTION + 0x10 * p);
+      a8[4 * p + 0] = 2.0f * u01f(r.x) - 1.0f;
+      a8[4 * p + 1] = 2.0f * u01f(r.y) - 1.0f;
+      a8[4 * p + 2] = 2.0f * u01f(r.z) - 1.0f;
+      a8[4 * p + 3] = 2.0f * u01f(r.w) - 1.0f;
+    } else {
+      float o[18];
+      if (p == 0) observe(w, o); else observe_two(w, o);
+      double inc;
+      if (io.opp_inc) inc = io.opp_inc[a * 2 + p];
+      else {
+        const int64_t ga = cfg.arena_offset + a;
+        U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), stepc, RNG_PHASE + 0x10 * p);
+        inc = 0.0 + (0.2 - 0.0) * u01d(r.x, r.y);
+      }
+      double ph = s.phase[p * s.n + a];
+      basic_opponent(pol == 2, w.keep_mode, ph, inc, o, &a8[4 * p]);
+      s.phase[p * s.n + a] = ph;
+    }
+  }
+  if (io.actions_out)
+    for (int k = 0; k < 8; ++k) io.actions_out[a * 8 + k] = a8[k];
+  // ---- HockeyEnv.step ----
+  const int was_done = w.done;
+  HK_TIC(T, 0);
+  presolve(w, a8);
+  HK_TIC(T, 1);
+  if (io.debug) {
+#ifdef HK_TRACE
+    float *d = io.debug + a * kTraceStride;
+#else
+    float *d = io.debug + a * 13;
+#endif
+    d[0] = w.d.fx[B_P1]; d[1] = w.d.fy[B_P1]; d[2] = w.d.fx[B_P2]; d[3] = w.d.fy[B_P2];
+    d[4] = w.d.fx[B_PK]; d[5] = w.d.fy[B_PK]; d[6] = w.d.tq[B_P1]; d[7] = w.d.tq[B_P2];
+    d[8] = w.d.ld[B_P1]; d[9] = w.d.ld[B_P2]; d[10] = w.d.ld[B_PK]; d[11] = w.d.ad[B_P1]; d[12] = w.d.ad[B_P2];
+  }
+  if (!(io.flags & 1)) {
+    world_step(w, T);
+  } else {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) { w.d.fx[b] = 0.0f; w.d.fy[b] = 0.0f; w.d.tq[b] = 0.0f; }
+  }
+  float o[18];
+  if (io.obs) {
+    observe(w, o);
+    for (int k = 0; k < 18; ++k) io.obs[a * 18 + k] = o[k];
+  }
+  if (w.time >= w.max_t) w.done = 1;
+  double info[4];
+  info_side<0>(w, info);
+  if (io.info) write_info(io.info, a, info);
+  if (io.reward) io.reward[a] = (float)(compute_reward(w) + info[1]);
+  if (io.obs2 || io.info2 || io.reward2) {
+    if (io.obs2) {
+      observe_two(w, o);
+      for (int k = 0; k < 18; ++k) io.obs2[a * 18 + k] = o[k];
+    }
+    double info2[4];
+    info_side<1>(w, info2);
+    if (io.info2) write_info(io.info2, a, info2);
+    if (io.reward2) io.reward2[a] = (float)(-compute_reward(w) + info2[1]);
+  }
+  if (io.done) io.done[a] = (uint8_t)w.done;
+  w.time += 1;
+  store_arena(w, s, a);
+  I(s, I_STEP, a) = (int)(stepc + 1);
+  HK_TIC(T, 5);
+  out.done_edge = (!was_done && w.done);
+  out.win1 = out.done_edge && w.winner == 1;
+  out.win2 = out.done_edge && w.winner == -1;
+  out.ntoi = w.n_toi;
+  out.ovf = w.overflow;
+  out.nbig = w.n_big;
+}
+
+
+HK_DEV void observe_lane(const DevState &s, const KCfg &cfg, int64_t a, float *obs, float *obs2) {
+  Arena w;
+  load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, nullptr, 0);
+  float o[18];
+  if (obs) {
+    observe(w, o);
+    for (int k = 0; k < 18; ++k) obs[a * 18 + k] = o[k];
+  }
+  if (obs2) {
+    observe_two(w, o);
+    for (int k = 0; k < 18; ++k) obs2[a * 18 + k] = o[k];
+  }
+}
+
+HK_DEV void get_state_lane(const DevState &s, int64_t a, float *st, int32_t *aux) {
+  for (int b = 0; b < 3; ++b) {
+    const int o = b * FB;
+    if (st) {
+      st[a * 18 + 6 * b + 0] = F(s, o + FB_PX, a);
+      st[a * 18 + 6 * b + 1] = F(s, o + FB_PY, a);
+      st[a * 18 + 6 * b + 2] = F(s, o + FB_A, a);
+      st[a * 18 + 6 * b + 3] = F(s, o + FB_VX, a);
+      st[a * 18 + 6 * b + 4] = F(s, o + FB_VY, a);
+      st[a * 18 + 6 * b + 5] = F(s, o + FB_W, a);
+    }
+  }
+  if (aux) {
+    aux[a * 5 + 0] = I(s, I_HAS1, a);
+    aux[a * 5 + 1] = I(s, I_HAS2, a);
+    aux[a * 5 + 2] = I(s, I_TIME, a);
+    aux[a * 5 + 3] = I(s, I_DONE, a);
+    aux[a * 5 + 4] = I(s, I_WINNER, a);
+  }
+}
+
+template <int B>
+HK_DEV void set_body_state(Arena &w, const float *x) {
+  set_transform<B>(w, V(x[0], x[1]), w.d.a[B]);
+  set_transform<B>(w, V(w.d.px[B], w.d.py[B]), x[2]);
+  set_linear_velocity<B>(w, V(x[3], x[4]));
+  set_angular_velocity<B>(w, x[5]);
+}
+
+// HockeyEnv.set_state (hockey_env.py:594-608) raw form: pybox2d setters, contacts untouched
+HK_DEV void set_state_lane(const DevState &s, const KCfg &cfg, int64_t a, const float *st, const int32_t *aux) {
+  Arena w;
+  load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, nullptr, 0);
+  if (st) {
+    const float *x = st + a * 18;
+    set_body_state<B_P1>(w, x);
+    set_body_state<B_P2>(w, x + 6);
+    set_body_state<B_PK>(w, x + 12);
+  }
+  if (aux) {
+    w.has1 = aux[a * 5 + 0];
+    w.has2 = aux[a * 5 + 1];
+    w.time = aux[a * 5 + 2];
+    w.done = aux[a * 5 + 3];
+    w.winner = aux[a * 5 + 4];
+  }
+  store_arena(w, s, a);
+}
+
+HK_DEV void init_lane(const DevState &s, const KCfg &cfg, int64_t a) {
+  for (int k = 0; k < NIF; ++k) I(s, k, a) = 0;
+  for (int k = 0; k < NFF; ++k) F(s, k, a) = 0.0f;
+  // HockeyEnv.__init__ sets one_starts = True and resets with one_starting=True (hockey_env.py:117,155);
+  // hk_create's first reset toggles this 0 -> 1.
+  I(s, I_ONE, a) = 0;
+  for (int p = 0; p < 2; ++p) {
+    const int64_t ga = cfg.arena_offset + a;
+    U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), 0, RNG_PHASE0 + 0x10 * p);
+    s.phase[p * s.n + a] = 0.0 + (kPiD - 0.0) * u01d(r.x, r.y);  // BasicOpponent.__init__ U(0, pi)
+  }
+}
+
+}  // namespace hk

@@ -63,7 +63,8 @@ enum {
   HK_CNT_GOALS_P1 = 2,  /* episodes won by player 1 */
   HK_CNT_GOALS_P2 = 3,  /* episodes won by player 2 */
   HK_CNT_TOI = 4,       /* solved time-of-impact events */
-  HK_CNT_OVERFLOW = 5   /* island / TOI capacity overflows (must stay 0) */
+  HK_CNT_OVERFLOW = 5,  /* island / TOI capacity overflows (must stay 0) */
+  HK_CNT_LARGE_ISLANDS = 6 /* solver calls with more contacts than the register fast path holds */
 };
 
 typedef struct hk_config {

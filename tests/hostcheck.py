@@ -1,0 +1,123 @@
+"""ctypes wrapper of libhockey_hostcheck.so: the kernel's per-arena source (hk_step.h and below) compiled
+for the host CPU.  TEST / DEBUG HARNESS ONLY -- the product package never loads it.
+
+It runs the exact device code paths (register arena, contact solver, TOI) lane by lane on the CPU, so the
+CPU suite can hold the kernel logic to the oracle bit for bit without a GPU, and gdb can step through it.
+"""
+import ctypes
+import os
+import subprocess
+from types import SimpleNamespace
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "hockey-env_amd", "csrc")
+LIB = os.environ.get("HKH_LIB") or os.path.join(ROOT, "hockey-env_amd", "hockey_amd", "_lib", "libhockey_hostcheck.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", CSRC, "hostcheck"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.environ.get("HKH_LIB"):
+            build()
+        L = ctypes.CDLL(LIB)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.hkh_create.restype = vp
+        L.hkh_create.argtypes = [i64, vp, ctypes.c_uint64, i64]
+        for name, n in (("hkh_destroy", 1), ("hkh_reset", 5), ("hkh_step", 2), ("hkh_get_state", 3),
+                        ("hkh_set_state", 4), ("hkh_observe", 3), ("hkh_counters", 2)):
+            getattr(L, name).restype = None
+            getattr(L, name).argtypes = [vp] * n
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class StepIO(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in ("actions", "opp_inc", "obs", "obs2", "reward", "reward2", "done",
+                                               "info", "info2", "actions_out", "debug")] + [("flags", ctypes.c_int32)]
+
+
+POLICY = {"external": 0, "random": 1, "weak": 2, "strong": 3}
+
+
+class HostVec:
+    """Same call shapes as hockey_amd.vec_env.VecHockeyEnv for the calls the parity tests make (numpy)."""
+
+    def __init__(self, n, keep_mode=True, mode=0, auto_reset=False, vel_ref=False,
+                 policies=("external", "external"), seed=0, arena_offset=0):
+        self.n = n
+        cfg = np.array([int(keep_mode), int(mode), int(auto_reset), int(vel_ref), POLICY[policies[0]],
+                        POLICY[policies[1]]], np.int32)
+        self._cfg = cfg
+        self.L = lib()
+        self.h = self.L.hkh_create(n, cfg.ctypes.data, seed, arena_offset)
+        self.L.hkh_reset(self.h, None, None, None, None)  # hk_create's device-placement reset
+
+    def close(self):
+        if self.h:
+            self.L.hkh_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self.L.hkh_reset(self.h, _p(m), None, None, None)
+
+    def reset_params(self, params, mask=None, max_t=None):
+        p = np.ascontiguousarray(params, np.float32)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        mt = None if max_t is None else np.ascontiguousarray(max_t, np.int32)
+        self.L.hkh_reset(self.h, _p(m), _p(p), _p(mt), None)
+
+    def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=False, skip_physics=False,
+             record_actions=False):
+        n = self.n
+        out = SimpleNamespace(obs=np.zeros((n, 18), np.float32), reward=np.zeros(n, np.float32),
+                              done=np.zeros(n, np.uint8), info=np.zeros((n, 4), np.float32))
+        io = StepIO()
+        a = None if actions is None else np.ascontiguousarray(actions, np.float32)
+        inc = None if opp_inc is None else np.ascontiguousarray(opp_inc, np.float64)
+        io.actions, io.opp_inc = _p(a), _p(inc)
+        io.obs, io.reward, io.done, io.info = _p(out.obs), _p(out.reward), _p(out.done), _p(out.info)
+        if with_agent_two:
+            out.obs2, out.reward2 = np.zeros((n, 18), np.float32), np.zeros(n, np.float32)
+            out.info2 = np.zeros((n, 4), np.float32)
+            io.obs2, io.reward2, io.info2 = _p(out.obs2), _p(out.reward2), _p(out.info2)
+        if debug:
+            out.debug = np.zeros((n, int(debug) if not isinstance(debug, bool) else 13), np.float32)
+            io.debug = _p(out.debug)
+        if record_actions:
+            out.actions = np.zeros((n, 8), np.float32)
+            io.actions_out = _p(out.actions)
+        io.flags = 1 if skip_physics else 0
+        self.L.hkh_step(self.h, ctypes.byref(io))
+        return out
+
+    def get_state(self):
+        st = np.zeros((self.n, 18), np.float32)
+        aux = np.zeros((self.n, 5), np.int32)
+        self.L.hkh_get_state(self.h, _p(st), _p(aux))
+        return st, aux
+
+    def set_state(self, state, aux=None, mask=None):
+        st = None if state is None else np.ascontiguousarray(state, np.float32)
+        ax = None if aux is None else np.ascontiguousarray(aux, np.int32)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self.L.hkh_set_state(self.h, _p(m), _p(st), _p(ax))
+
+    def counters(self):
+        c = np.zeros(16, np.uint64)
+        self.L.hkh_counters(self.h, _p(c))
+        return c

@@ -1,0 +1,91 @@
+"""The kernel's per-arena source (hk_step.h -> hk_arena.h / hk_solver.h / hk_geom.h), compiled for the host
+CPU by tests/hostcheck.py, held bit-for-bit to the oracle -- on the CPU, without a GPU.
+
+This catches logic errors in the device code before a GPU run; the GPU parity tests (test_gpu_parity.py)
+then hold the gfx950 binary of the same source to the same oracle.  The harness is test infrastructure
+(never loaded by the product package).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from hockey_amd.placement import np_random, placement
+
+from hostcheck import HostVec
+
+
+def _f32(x):
+    return np.asarray(x, np.float64).astype(np.float32)
+
+
+def _lockstep(oracle, mode, n, steps, seed):
+    keep = True
+    env = HostVec(n, keep_mode=keep, mode=mode)
+    params = np.zeros((n, 6), np.float32)
+    for i in range(n):
+        rng, _ = np_random(seed * 100_000 + i)
+        params[i], max_t = placement(mode, bool(i % 2), rng)
+    env.reset_params(params)
+    ws = []
+    for i in range(n):
+        w = oracle.OracleWorld(keep, mode)
+        w.reset(params[i], max_t)
+        ws.append(w)
+    rng = np.random.default_rng(seed)
+    phases = rng.uniform(0, np.pi, (n, 2))
+    obs = np.stack([w.obs() for w in ws]).astype(np.float64)
+    obs2 = np.stack([w.obs_two() for w in ws]).astype(np.float64)
+    n_toi = 0
+    for t in range(steps):
+        acts = rng.uniform(-1, 1, (n, 8)).astype(np.float32)
+        for i in range(0, n, 2):  # half the arenas: strong-vs-strong BasicOpponent (contacts, shots, goals)
+            a1, phases[i, 0] = oracle.basic_opponent(0, 1, phases[i, 0], 0.1, obs[i])
+            a2, phases[i, 1] = oracle.basic_opponent(0, 1, phases[i, 1], 0.1, obs2[i])
+            acts[i] = np.concatenate([a1, a2]).astype(np.float32)
+        res = env.step(acts, with_agent_two=True)
+        for i, w in enumerate(ws):
+            o, r, d, info, _ = w.step(acts[i])
+            n_toi += w.stats()[1]
+            o2 = w.obs_two()
+            i2, r2 = w.info_two()
+            checks = (("obs", np.array_equal(res.obs[i], o)), ("obs2", np.array_equal(res.obs2[i], o2)),
+                      ("reward", res.reward[i] == np.float32(r)), ("reward2", res.reward2[i] == np.float32(r2)),
+                      ("done", bool(res.done[i]) == d), ("info", np.array_equal(res.info[i], _f32(info))))
+            for name, ok in checks:
+                if not ok:
+                    return {"step": t, "arena": i, "field": name}
+            obs[i], obs2[i] = o, o2
+    st, _ = env.get_state()
+    for i, w in enumerate(ws):
+        assert np.array_equal(st[i], w.get_raw()[0]), i
+    out = {"n_toi": n_toi, "counters": env.counters()}
+    env.close()
+    return out
+
+
+@pytest.mark.parametrize("mode,seed", [(0, 1), (1, 3), (2, 4)])
+def test_kernel_source_lockstep_vs_oracle(oracle, mode, seed):
+    out = _lockstep(oracle, mode, n=48, steps=200, seed=seed)
+    assert "field" not in out, out
+    if mode == 0:
+        assert out["n_toi"] > 0
+
+
+def test_large_island_solver_vs_oracle(oracle, monkeypatch):
+    """HK_ABLATE=1 routes every island / TOI solve through the HBM slot file (HbmSlots, the path of islands
+    with more contacts than the register slots) -- it must be bit-identical as well."""
+    monkeypatch.setenv("HK_ABLATE", "1")
+    out = _lockstep(oracle, 1, n=32, steps=150, seed=3)
+    assert "field" not in out, out
+    assert out["counters"][6] > 0  # large-island solves were taken
+
+
+def test_fused_opponents_autoreset_run(oracle):
+    """Fused strong/weak BasicOpponent with device auto-reset: counters consistent, no overflow."""
+    env = HostVec(256, policies=("strong", "weak"), auto_reset=True, seed=7)
+    for _ in range(300):
+        env.step(None)
+    c = env.counters()
+    assert c[0] == 256 * 300 and c[5] == 0
+    assert c[1] > 0 and c[2] + c[3] <= c[1]
