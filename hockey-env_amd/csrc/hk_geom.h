@@ -95,19 +95,18 @@ HK_DEV void find_incident_edge(ClipV c[2], const Fixture &p1, xform xf1, int edg
   c[1].id = cf_id(edge1, i2, 1, 0);
 }
 
+// b2ClipSegmentToLine, written with selects (no dynamically indexed private arrays)
 HK_DEV int clip_segment(ClipV out[2], const ClipV in[2], v2 normal, float offset, int vA) {
-  int n = 0;
-  float d0 = dot(normal, in[0].v) - offset;
-  float d1 = dot(normal, in[1].v) - offset;
-  if (d0 <= 0.0f) out[n++] = in[0];
-  if (d1 <= 0.0f) out[n++] = in[1];
-  if (d0 * d1 < 0.0f) {
-    float interp = d0 / (d0 - d1);
-    out[n].v = vadd(in[0].v, vs(interp, vsub(in[1].v, in[0].v)));
-    out[n].id = cf_id(vA, (in[0].id >> 8) & 0xffu, 0, 1);
-    ++n;
-  }
-  return n;
+  const float d0 = dot(normal, in[0].v) - offset;
+  const float d1 = dot(normal, in[1].v) - offset;
+  const bool k0 = d0 <= 0.0f, k1 = d1 <= 0.0f, cross = d0 * d1 < 0.0f;
+  const float interp = d0 / (d0 - d1);  // used only when the segment crosses the line
+  ClipV ix;
+  ix.v = vadd(in[0].v, vs(interp, vsub(in[1].v, in[0].v)));
+  ix.id = cf_id(vA, (in[0].id >> 8) & 0xffu, 0, 1);
+  out[0] = k0 ? in[0] : (k1 ? in[1] : ix);
+  out[1] = (k0 && k1) ? in[1] : ix;
+  return (int)k0 + (int)k1 + (int)cross;
 }
 
 HK_DEV void collide_polygons(Manifold &m, const Fixture &pA, xform xfA, const Fixture &pB, xform xfB) {
@@ -147,18 +146,24 @@ HK_DEV void collide_polygons(Manifold &m, const Fixture &pA, xform xfA, const Fi
   if (np < 2) return;
   m.ln = ln;
   m.lp = pp;
-  int pc = 0;
+  v2 q[2];
+  uint32_t qid[2];
+  bool keep[2];
+#pragma unroll
   for (int i = 0; i < 2; ++i) {
-    float sep = dot(normal, cp2[i].v) - front;
-    if (sep <= total) {
-      m.pt_lp[pc] = mulT_xv(xf2, cp2[i].v);
-      uint32_t id = cp2[i].id;
-      if (flip) id = cf_id((id >> 8) & 0xffu, id & 0xffu, (id >> 24) & 0xffu, (id >> 16) & 0xffu);
-      m.id[pc] = id;
-      ++pc;
-    }
+    const float sep = dot(normal, cp2[i].v) - front;
+    keep[i] = sep <= total;
+    q[i] = mulT_xv(xf2, cp2[i].v);
+    uint32_t id = cp2[i].id;
+    if (flip) id = cf_id((id >> 8) & 0xffu, id & 0xffu, (id >> 24) & 0xffu, (id >> 16) & 0xffu);
+    qid[i] = id;
   }
-  m.count = pc;
+  // kept points, in order
+  m.pt_lp[0] = keep[0] ? q[0] : q[1];
+  m.id[0] = keep[0] ? qid[0] : qid[1];
+  m.pt_lp[1] = q[1];
+  m.id[1] = qid[1];
+  m.count = (int)keep[0] + (int)keep[1];
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -7,6 +7,7 @@
 // give the float32 mass, centre and inertia.  The contact pair table is the category/mask filter of
 // SURVEY.md A.3 in a fixed canonical order.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "hk_kernels.h"
@@ -211,6 +212,8 @@ void build_scene(Scene &sc) {
     sc.friction[p] = std::sqrt(fA.friction * fB.friction);                      // b2MixFriction
     sc.restitution[p] = fA.restitution > fB.restitution ? fA.restitution : fB.restitution;  // b2MixRestitution
     sc.manslot[p] = sc.sensor[p] ? -1 : slot++;
+    // the solver derives radii from this layout (hk_solver.h pair_rA / pair_rB)
+    if (fA.radius != kPolyRadius || (fB.body != B_PK && fB.radius != kPolyRadius) || fA.body == B_PK) std::abort();
   }
   for (int f = 0; f < NF; ++f) {
     const Fixture &fx = sc.fx[f];

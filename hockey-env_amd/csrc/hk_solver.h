@@ -13,17 +13,27 @@ namespace hk {
 
 
 
+// One contact of the solver.  Only what the velocity iterations touch lives here (36 words); the
+// position-phase geometry (manifold points / normal, local centres, radii, static origins) is re-read from
+// the in-place HBM manifold and the scene when a position pass or InitializeVelocityConstraints needs it,
+// so it is not live in registers across the 180-iteration velocity loop.
 struct FSlot {
-  int p, bA, bB, vcount, pcount, type, isl;
-  float mA, mB, iA, iB, fr, re;
-  float sAx, sAy;  // origin of a static body A (bA == 3)
+  int bits;  // pair | island << 5 | bodyA << 7 | bodyB << 11 | vcount << 15 | pcount << 17 | type << 19
+  float mA, mB, iA, iB, fr;
   float nx, ny;
   float rAx[2], rAy[2], rBx[2], rBy[2], ni[2], ti[2], nm[2], tm[2], bias[2];
-  float Kxx, Kxy, Kyx, Kyy, Nxx, Nxy, Nyx, Nyy;
-  float lpsx[2], lpsy[2], lnx, lny, lpx, lpy, lcAx, lcAy, lcBx, lcBy, rA, rB;
-  uint32_t sn[4];  // impulse snapshot for the periodic early exit (velocity_iterations)
+  float Kxx, Kxy, Kyy, Nxx, Nxy, Nyy;  // K and its inverse are symmetric (Box2D stores ex.y == ey.x)
+  uint32_t sn[4];                       // impulse snapshot for the periodic early exit (velocity_iterations)
 };
 constexpr int kSlotWords = (int)(sizeof(FSlot) / 4);
+
+HK_DEV int fs_pair(const FSlot &s) { return s.bits & 31; }
+HK_DEV int fs_isl(const FSlot &s) { return (s.bits >> 5) & 3; }
+HK_DEV int fs_bA(const FSlot &s) { return (s.bits >> 7) & 15; }
+HK_DEV int fs_bB(const FSlot &s) { return (s.bits >> 11) & 15; }
+HK_DEV int fs_vcount(const FSlot &s) { return (s.bits >> 15) & 3; }
+HK_DEV int fs_pcount(const FSlot &s) { return (s.bits >> 17) & 3; }
+HK_DEV int fs_type(const FSlot &s) { return (s.bits >> 19) & 3; }
 
 HK_DEV void get_vel(const Dyn &B, int b, v2 &v, float &w) {
   v = V(pick(B.vx, b, 0.0f), pick(B.vy, b, 0.0f));
@@ -34,9 +44,15 @@ HK_DEV void set_vel(Dyn &B, int b, v2 v, float w) {
   place(B.vy, b, v.y);
   place(B.w, b, w);
 }
-HK_DEV void get_pos(const Dyn &B, int b, float sx, float sy, v2 &c, float &a) {
-  c = V(pick(B.cx, b, sx), pick(B.cy, b, sy));
-  a = pick(B.a, b, 0.0f);
+// position of body b (a static body sits at its origin with angle 0)
+HK_DEV void get_pos(const Dyn &B, int b, v2 &c, float &a) {
+  if (b < 3) {
+    c = V(pick(B.cx, b, 0.0f), pick(B.cy, b, 0.0f));
+    a = pick(B.a, b, 0.0f);
+  } else {
+    c = V(SC.spx[b], SC.spy[b]);
+    a = 0.0f;
+  }
 }
 HK_DEV void set_pos(Dyn &B, int b, v2 c, float a) {
   place(B.cx, b, c.x);
@@ -44,95 +60,102 @@ HK_DEV void set_pos(Dyn &B, int b, v2 c, float a) {
   place(B.a, b, a);
 }
 
+// fixture radii of a pair: fixture A is always a polygon (walls, goals, players); B is a player polygon or
+// the puck circle (build_scene checks this layout)
+HK_DEV float pair_rA() { return kPolyRadius; }
+HK_DEV float pair_rB(int bB) { return bB == B_PK ? SC.fx[F_PK].radius : kPolyRadius; }
+
+// position-phase view of a contact's manifold (read in place from HBM)
+struct ManGeo {
+  int type, count;
+  v2 ln, lp, pt[2];
+};
+HK_DEV ManGeo man_geo(const Arena &w, int p) {
+  const int slot = SC.manslot[p];
+  ManGeo g;
+  const int meta = __float_as_int(MF(w, slot, M_META));
+  g.count = meta & 0xff;
+  g.type = meta >> 8;
+  g.ln = V(MF(w, slot, M_LNX), MF(w, slot, M_LNY));
+  g.lp = V(MF(w, slot, M_LPX), MF(w, slot, M_LPY));
+  g.pt[0] = V(MF(w, slot, M_P0X), MF(w, slot, M_P0Y));
+  g.pt[1] = g.count > 1 ? V(MF(w, slot, M_P1X), MF(w, slot, M_P1Y)) : V(0.0f, 0.0f);
+  return g;
+}
+
 // b2ContactSolver constructor for one contact
 HK_DEV void fslot_load(FSlot &s, const Arena &w, int p, int warm, int isl) {
   const int pa = SC.pbodyA[p], pb = SC.pbodyB[p];
   const int slot = SC.manslot[p];
-  s.p = p;
-  s.isl = isl;
-  s.bA = pa < 3 ? pa : 3;
-  s.bB = pb;  // always dynamic
-  s.fr = SC.friction[p];
-  s.re = SC.restitution[p];
-  s.mA = inv_mass(pa); s.mB = inv_mass(pb); s.iA = inv_inertia(pa); s.iB = inv_inertia(pb);
-  s.sAx = SC.spx[pa];
-  s.sAy = SC.spy[pa];
   const int meta = __float_as_int(MF(w, slot, M_META));
-  s.vcount = meta & 0xff;
-  s.pcount = s.vcount;
-  s.type = meta >> 8;
-  s.Kxx = s.Kxy = s.Kyx = s.Kyy = 0.0f;
-  s.Nxx = s.Nxy = s.Nyx = s.Nyy = 0.0f;
-  s.lnx = MF(w, slot, M_LNX); s.lny = MF(w, slot, M_LNY); s.lpx = MF(w, slot, M_LPX); s.lpy = MF(w, slot, M_LPY);
-  const v2 lcA = local_center(pa), lcB = local_center(pb);
-  s.lcAx = lcA.x; s.lcAy = lcA.y; s.lcBx = lcB.x; s.lcBy = lcB.y;
-  s.rA = SC.fx[SC.pairA[p]].radius;
-  s.rB = SC.fx[SC.pairB[p]].radius;
+  const int count = meta & 0xff, type = meta >> 8;
+  s.bits = p | (isl << 5) | (pa << 7) | (pb << 11) | (count << 15) | (count << 17) | (type << 19);
+  s.fr = SC.friction[p];
+  s.mA = inv_mass(pa); s.mB = inv_mass(pb); s.iA = inv_inertia(pa); s.iB = inv_inertia(pb);
+  s.Kxx = s.Kxy = s.Kyy = 0.0f;
+  s.Nxx = s.Nxy = s.Nyy = 0.0f;
+  s.nx = s.ny = 0.0f;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const bool on = j < s.pcount;
+    const bool on = j < count;
     const int o = M_P0X + j * 5;
     s.ni[j] = on && warm ? 1.0f * MF(w, slot, o + 3) : 0.0f;
     s.ti[j] = on && warm ? 1.0f * MF(w, slot, o + 4) : 0.0f;
     s.rAx[j] = s.rAy[j] = s.rBx[j] = s.rBy[j] = 0.0f;
     s.nm[j] = s.tm[j] = s.bias[j] = 0.0f;
-    s.lpsx[j] = on ? MF(w, slot, o + 0) : 0.0f;
-    s.lpsy[j] = on ? MF(w, slot, o + 1) : 0.0f;
   }
+  s.sn[0] = s.sn[1] = s.sn[2] = s.sn[3] = 0u;
 }
 
 // InitializeVelocityConstraints for one contact
-HK_DEV void fslot_init_velocity(FSlot &s, const Dyn &B) {
+HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
+  const Dyn &B = w.d;
   const float mA = s.mA, mB = s.mB, iA = s.iA, iB = s.iB;
+  const int bA = fs_bA(s), bB = fs_bB(s), p = fs_pair(s);
+  const float rAr = pair_rA(), rBr = pair_rB(bB);
   v2 cA, cB, vA, vB;
   float aA, aB, wA, wB;
-  get_pos(B, s.bA, s.sAx, s.sAy, cA, aA);
-  get_pos(B, s.bB, 0.0f, 0.0f, cB, aB);
-  get_vel(B, s.bA, vA, wA);
-  get_vel(B, s.bB, vB, wB);
+  get_pos(B, bA, cA, aA);
+  get_pos(B, bB, cB, aB);
+  get_vel(B, bA, vA, wA);
+  get_vel(B, bB, vB, wB);
   xform xA, xB;
   xA.q = rot_set(aA);
   xB.q = rot_set(aB);
-  xA.p = vsub(cA, mul_rv(xA.q, V(s.lcAx, s.lcAy)));
-  xB.p = vsub(cB, mul_rv(xB.q, V(s.lcBx, s.lcBy)));
+  xA.p = vsub(cA, mul_rv(xA.q, local_center(bA)));
+  xB.p = vsub(cB, mul_rv(xB.q, local_center(bB)));
   // b2WorldManifold::Initialize
+  const ManGeo m = man_geo(w, p);
   v2 normal, pts[2];
-  {
-    Manifold m;
-    m.type = s.type;
-    m.count = s.pcount;
-    m.ln = V(s.lnx, s.lny);
-    m.lp = V(s.lpx, s.lpy);
-    m.pt_lp[0] = V(s.lpsx[0], s.lpsy[0]);
-    m.pt_lp[1] = V(s.lpsx[1], s.lpsy[1]);
-    if (m.type == 1) {
-      normal = mul_rv(xA.q, m.ln);
-      v2 plane = mul_xv(xA, m.lp);
+  if (m.type == 1) {
+    normal = mul_rv(xA.q, m.ln);
+    v2 plane = mul_xv(xA, m.lp);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        v2 clip = mul_xv(xB, m.pt_lp[i]);
-        v2 ca = vadd(clip, vs(s.rA - dot(vsub(clip, plane), normal), normal));
-        v2 cb = vsub(clip, vs(s.rB, normal));
-        pts[i] = vs(0.5f, vadd(ca, cb));
-      }
-    } else {
-      normal = mul_rv(xB.q, m.ln);
-      v2 plane = mul_xv(xB, m.lp);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        v2 clip = mul_xv(xA, m.pt_lp[i]);
-        v2 cb = vadd(clip, vs(s.rB - dot(vsub(clip, plane), normal), normal));
-        v2 ca = vsub(clip, vs(s.rA, normal));
-        pts[i] = vs(0.5f, vadd(ca, cb));
-      }
-      normal = vneg(normal);
+    for (int i = 0; i < 2; ++i) {
+      v2 clip = mul_xv(xB, m.pt[i]);
+      v2 ca = vadd(clip, vs(rAr - dot(vsub(clip, plane), normal), normal));
+      v2 cb = vsub(clip, vs(rBr, normal));
+      pts[i] = vs(0.5f, vadd(ca, cb));
     }
+  } else {
+    normal = mul_rv(xB.q, m.ln);
+    v2 plane = mul_xv(xB, m.lp);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      v2 clip = mul_xv(xA, m.pt[i]);
+      v2 cb = vadd(clip, vs(rBr - dot(vsub(clip, plane), normal), normal));
+      v2 ca = vsub(clip, vs(rAr, normal));
+      pts[i] = vs(0.5f, vadd(ca, cb));
+    }
+    normal = vneg(normal);
   }
   s.nx = normal.x;
   s.ny = normal.y;
+  const float re = SC.restitution[p];
+  const int vcount = fs_vcount(s);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    if (j < s.vcount) {
+    if (j < vcount) {
       v2 rA = vsub(pts[j], cA), rB = vsub(pts[j], cB);
       s.rAx[j] = rA.x; s.rAy[j] = rA.y; s.rBx[j] = rB.x; s.rBy[j] = rB.y;
       float rnA = crs(rA, normal), rnB = crs(rB, normal);
@@ -144,10 +167,10 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Dyn &B) {
       s.tm[j] = kT > 0.0f ? 1.0f / kT : 0.0f;
       s.bias[j] = 0.0f;
       float vRel = dot(normal, vsub(vsub(vadd(vB, crs_sv(wB, rB)), vA), crs_sv(wA, rA)));
-      if (vRel < -kVelocityThreshold) s.bias[j] = -s.re * vRel;
+      if (vRel < -kVelocityThreshold) s.bias[j] = -re * vRel;
     }
   }
-  if (s.vcount == 2) {
+  if (vcount == 2) {
     v2 r1A = V(s.rAx[0], s.rAy[0]), r1B = V(s.rBx[0], s.rBy[0]);
     v2 r2A = V(s.rAx[1], s.rAy[1]), r2B = V(s.rBx[1], s.rBy[1]);
     float rn1A = crs(r1A, normal), rn1B = crs(r1B, normal);
@@ -156,27 +179,29 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Dyn &B) {
     float k22 = mA + mB + iA * rn2A * rn2A + iB * rn2B * rn2B;
     float k12 = mA + mB + iA * rn1A * rn2A + iB * rn1B * rn2B;
     if (k11 * k11 < 1000.0f * (k11 * k22 - k12 * k12)) {
-      s.Kxx = k11; s.Kxy = k12; s.Kyx = k12; s.Kyy = k22;
-      float a = s.Kxx, b = s.Kyx, c = s.Kxy, d = s.Kyy;
+      s.Kxx = k11; s.Kxy = k12; s.Kyy = k22;
+      float a = s.Kxx, b = s.Kxy, c = s.Kxy, d = s.Kyy;
       float det = a * d - b * c;
       if (det != 0.0f) det = 1.0f / det;
-      s.Nxx = det * d; s.Nyx = -det * b;
-      s.Nxy = -det * c; s.Nyy = det * a;
+      s.Nxx = det * d;
+      s.Nxy = -det * c;
+      s.Nyy = det * a;
     } else {
-      s.vcount = 1;
+      s.bits = (s.bits & ~(3 << 15)) | (1 << 15);  // vcount = 1
     }
   }
 }
 
 HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
+  const int bA = fs_bA(s), bB = fs_bB(s), vcount = fs_vcount(s);
   v2 vA, vB;
   float wA, wB;
-  get_vel(B, s.bA, vA, wA);
-  get_vel(B, s.bB, vB, wB);
+  get_vel(B, bA, vA, wA);
+  get_vel(B, bB, vB, wB);
   const v2 normal = V(s.nx, s.ny), tangent = crs_vs(normal, 1.0f);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    if (j < s.vcount) {
+    if (j < vcount) {
       v2 P = vadd(vs(s.ni[j], normal), vs(s.ti[j], tangent));
       wA -= s.iA * crs(V(s.rAx[j], s.rAy[j]), P);
       vA = vsub(vA, vs(s.mA, P));
@@ -184,21 +209,22 @@ HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
       vB = vadd(vB, vs(s.mB, P));
     }
   }
-  set_vel(B, s.bA, vA, wA);
-  set_vel(B, s.bB, vB, wB);
+  set_vel(B, bA, vA, wA);
+  set_vel(B, bB, vB, wB);
 }
 
 // one b2ContactSolver::SolveVelocityConstraints pass over one contact
 HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
   const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
+  const int bA = fs_bA(s), bB = fs_bB(s), vcount = fs_vcount(s);
   v2 vA, vB;
   float wA, wB;
-  get_vel(B, s.bA, vA, wA);
-  get_vel(B, s.bB, vB, wB);
+  get_vel(B, bA, vA, wA);
+  get_vel(B, bB, vB, wB);
   const v2 normal = V(s.nx, s.ny), tangent = crs_vs(normal, 1.0f);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    if (j < s.vcount) {
+    if (j < vcount) {
       const v2 rA = V(s.rAx[j], s.rAy[j]), rB = V(s.rBx[j], s.rBy[j]);
       v2 dv = vsub(vsub(vadd(vB, crs_sv(wB, rB)), vA), crs_sv(wA, rA));
       float vt = dot(dv, tangent) - 0.0f;
@@ -214,7 +240,7 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
       wB += iB * crs(rB, P);
     }
   }
-  if (s.vcount == 1) {
+  if (vcount == 1) {
     const v2 rA = V(s.rAx[0], s.rAy[0]), rB = V(s.rBx[0], s.rBy[0]);
     v2 dv = vsub(vsub(vadd(vB, crs_sv(wB, rB)), vA), crs_sv(wA, rA));
     float vn = dot(dv, normal);
@@ -237,8 +263,8 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
     v2 b;
     b.x = vn1 - s.bias[0];
     b.y = vn2 - s.bias[1];
-    b = vsub(b, V(s.Kxx * a.x + s.Kyx * a.y, s.Kxy * a.x + s.Kyy * a.y));
-    v2 x = vneg(V(s.Nxx * b.x + s.Nyx * b.y, s.Nxy * b.x + s.Nyy * b.y));
+    b = vsub(b, V(s.Kxx * a.x + s.Kxy * a.y, s.Kxy * a.x + s.Kyy * a.y));
+    v2 x = vneg(V(s.Nxx * b.x + s.Nxy * b.y, s.Nxy * b.x + s.Nyy * b.y));
     int ok = 0;
     if (x.x >= 0.0f && x.y >= 0.0f) ok = 1;
     if (!ok) {
@@ -250,7 +276,7 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
     if (!ok) {
       x.x = 0.0f;
       x.y = -s.nm[1] * b.y;
-      vn1 = s.Kyx * x.y + b.x;
+      vn1 = s.Kxy * x.y + b.x;
       if (x.y >= 0.0f && vn1 >= 0.0f) ok = 1;
     }
     if (!ok) {
@@ -271,38 +297,44 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
       s.ni[1] = x.y;
     }
   }
-  set_vel(B, s.bA, vA, wA);
-  set_vel(B, s.bB, vB, wB);
+  set_vel(B, bA, vA, wA);
+  set_vel(B, bB, vB, wB);
 }
 
-// one NGS position pass over one contact; mass scales select SolveTOIPositionConstraints
-HK_DEV float fslot_solve_position(const FSlot &s, Dyn &B, float baum, float mA, float iA, float mB, float iB,
-                                  float minSep) {
+// one NGS position pass over one contact (b2ContactSolver::SolvePositionConstraints body).  In this scene
+// SolveTOIPositionConstraints' mass gating is the identity (see solve_toi), so one routine serves both.
+HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float minSep) {
+  Dyn &B = w.d;
+  const float mA = s.mA, mB = s.mB, iA = s.iA, iB = s.iB;
+  const int bA = fs_bA(s), bB = fs_bB(s), pcount = fs_pcount(s);
+  const ManGeo m = man_geo(w, fs_pair(s));
+  const v2 lcA = local_center(bA), lcB = local_center(bB);
+  const float rAr = pair_rA(), rBr = pair_rB(bB);
   v2 cA, cB;
   float aA, aB;
-  get_pos(B, s.bA, s.sAx, s.sAy, cA, aA);
-  get_pos(B, s.bB, 0.0f, 0.0f, cB, aB);
+  get_pos(B, bA, cA, aA);
+  get_pos(B, bB, cB, aB);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    if (j < s.pcount) {
+    if (j < pcount) {
       xform xA, xB;
       xA.q = rot_set(aA);
       xB.q = rot_set(aB);
-      xA.p = vsub(cA, mul_rv(xA.q, V(s.lcAx, s.lcAy)));
-      xB.p = vsub(cB, mul_rv(xB.q, V(s.lcBx, s.lcBy)));
+      xA.p = vsub(cA, mul_rv(xA.q, lcA));
+      xB.p = vsub(cB, mul_rv(xB.q, lcB));
       v2 normal, point;
       float sep;
-      if (s.type == 1) {
-        normal = mul_rv(xA.q, V(s.lnx, s.lny));
-        v2 plane = mul_xv(xA, V(s.lpx, s.lpy));
-        v2 clip = mul_xv(xB, V(s.lpsx[j], s.lpsy[j]));
-        sep = dot(vsub(clip, plane), normal) - s.rA - s.rB;
+      if (m.type == 1) {
+        normal = mul_rv(xA.q, m.ln);
+        v2 plane = mul_xv(xA, m.lp);
+        v2 clip = mul_xv(xB, m.pt[j]);
+        sep = dot(vsub(clip, plane), normal) - rAr - rBr;
         point = clip;
       } else {
-        normal = mul_rv(xB.q, V(s.lnx, s.lny));
-        v2 plane = mul_xv(xB, V(s.lpx, s.lpy));
-        v2 clip = mul_xv(xA, V(s.lpsx[j], s.lpsy[j]));
-        sep = dot(vsub(clip, plane), normal) - s.rA - s.rB;
+        normal = mul_rv(xB.q, m.ln);
+        v2 plane = mul_xv(xB, m.lp);
+        v2 clip = mul_xv(xA, m.pt[j]);
+        sep = dot(vsub(clip, plane), normal) - rAr - rBr;
         point = clip;
         normal = vneg(normal);
       }
@@ -319,8 +351,8 @@ HK_DEV float fslot_solve_position(const FSlot &s, Dyn &B, float baum, float mA, 
       aB += iB * crs(rB, Pv);
     }
   }
-  if (s.bA < 3) set_pos(B, s.bA, cA, aA);
-  set_pos(B, s.bB, cB, aB);
+  if (bA < 3) set_pos(B, bA, cA, aA);
+  set_pos(B, bB, cB, aB);
   return minSep;
 }
 
@@ -334,25 +366,24 @@ HK_DEV float fslot_solve_position(const FSlot &s, Dyn &B, float baum, float mA, 
 // solves become periodic, most within 4-12 iterations.
 // ------------------------------------------------------------------------------------------------
 // Slot files.  Both run fn(slot, i) over the first nc slots in order (Gauss-Seidel order matters).
-//   RegSlots: kFastC slots in registers, loops fully unrolled (compile-time slot indices) -- the hot path.
+//   RegSlots<C>: C slots in registers, loops fully unrolled (compile-time slot indices) -- the hot path
+//             (islands: C = kIslandC, TOI mini-islands: C = kToiC).
 //   HbmSlots: up to kBigC slots in the HBM workspace DevState::ws ([slot][word][arena], lane-contiguous);
 //             each visit loads one slot into registers, runs fn and writes it back.  Used by the rare
 //             large islands (~1e-5 of arena-steps) so they neither inflate the hot path's register
 //             budget nor use private (scratch) memory.
+template <int C>
 struct RegSlots {
-  FSlot s[kFastC];
+  FSlot s[C];
   template <typename Fn>
   HK_DEV void each(int nc, Fn &&fn) {
 #pragma unroll
-    for (int i = 0; i < kFastC; ++i)
+    for (int i = 0; i < C; ++i)
       if (i < nc) fn(s[i], i);
   }
   HK_DEV void set_pair(int nc, int p, int isl) {
 #pragma unroll
-    for (int q = 0; q < kFastC; ++q) {
-      s[q].p = (q == nc) ? p : s[q].p;
-      s[q].isl = (q == nc) ? isl : s[q].isl;
-    }
+    for (int q = 0; q < C; ++q) s[q].bits = (q == nc) ? (p | (isl << 5)) : s[q].bits;
   }
 };
 
@@ -374,14 +405,11 @@ struct HbmSlots {
     }
   }
   HK_DEV void set_pair(int nc, int p, int isl) {
-    if (nc < kBigC) {
-      word(nc, (int)(offsetof(FSlot, p) / 4)) = __int_as_float(p);
-      word(nc, (int)(offsetof(FSlot, isl) / 4)) = __int_as_float(isl);
-    }
+    if (nc < kBigC) word(nc, (int)(offsetof(FSlot, bits) / 4)) = __int_as_float(p | (isl << 5));
   }
 };
 template <typename SL> struct SlotCap;
-template <> struct SlotCap<RegSlots> { static constexpr int value = kFastC; };
+template <int C> struct SlotCap<RegSlots<C>> { static constexpr int value = C; };
 template <> struct SlotCap<HbmSlots> { static constexpr int value = kBigC; };
 
 // 180 velocity iterations over nc slots, with the exact periodic early exit
@@ -390,7 +418,6 @@ HK_DEV void velocity_iterations(SL &S, Dyn &B, int nc) {
   uint32_t sb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) sb[k] = 0u;
-  S.each(nc, [&](FSlot &s, int) { s.sn[0] = s.sn[1] = s.sn[2] = s.sn[3] = 0u; });
   bool active = nc > 0;
   for (int it = 0; it < kVelIters && active; ++it) {
     S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
@@ -419,10 +446,11 @@ HK_DEV void velocity_iterations(SL &S, Dyn &B, int nc) {
 }
 
 HK_DEV void fslot_store(const FSlot &s, Arena &w) {
-  const int slot = SC.manslot[s.p];
+  const int slot = SC.manslot[fs_pair(s)];
+  const int vcount = fs_vcount(s);
 #pragma unroll
   for (int j = 0; j < 2; ++j)
-    if (j < s.vcount) {
+    if (j < vcount) {
       MF(w, slot, M_P0X + j * 5 + 3) = s.ni[j];
       MF(w, slot, M_P0X + j * 5 + 4) = s.ti[j];
     }

@@ -173,11 +173,15 @@ HK_DEV void device_placement(uint64_t seed, int64_t a, uint32_t episode, int mod
   const double W = 10.0, H = 8.0;
   U4 r0 = philox(seed, (uint32_t)a, (uint32_t)(a >> 32), episode, RNG_RESET);
   U4 r1 = philox(seed, (uint32_t)a, (uint32_t)(a >> 32), episode, RNG_RESET + 0x100);
-  double u[4] = {u01d(r0.x, r0.y), u01d(r0.z, r0.w), u01d(r1.x, r1.y), u01d(r1.z, r1.w)};
+  const double u0 = u01d(r0.x, r0.y), u1 = u01d(r0.z, r0.w), u2 = u01d(r1.x, r1.y), u3 = u01d(r1.z, r1.w);
   U4 r2 = philox(seed, (uint32_t)a, (uint32_t)(a >> 32), episode, RNG_RESET + 0x200);
-  double u4 = u01d(r2.x, r2.y);
-  int k = 0;
-  auto unif = [&](double lo, double hi) { double x = (k < 4) ? u[k] : u4; ++k; return lo + (hi - lo) * x; };
+  const double u4 = u01d(r2.x, r2.y);
+  int k = 0;  // k-th uniform of this reset (a select chain: no indexed private array)
+  auto unif = [&](double lo, double hi) {
+    const double x = k == 0 ? u0 : (k == 1 ? u1 : (k == 2 ? u2 : (k == 3 ? u3 : u4)));
+    ++k;
+    return lo + (hi - lo) * x;
+  };
   max_t = mode == 0 ? 250 : 80;
   double p2x = 4 * W / 5, p2y = H / 2;
   if (mode != 0) {

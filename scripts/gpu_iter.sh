@@ -1,0 +1,11 @@
+#!/bin/bash
+# Quick GPU iteration: parity tests, bench (no CPU baseline), phase timers.  Stops at the first failure.
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 300 --warmup 200 > gpurun_out/bench.log 2>&1
+grep -o '"value": [0-9.e+]*\|"kernel_avg_ms": [0-9.e+]*' gpurun_out/bench.log
+timeout -k 10 300 python scripts/phase_timers.py 65536 strong > gpurun_out/phase.log 2>&1
+grep -v amdgpu.ids gpurun_out/phase.log
