@@ -65,6 +65,23 @@ def cpu_baseline(policy, n_arenas):
                       f"auto-reset) on the C restatement of HockeyEnv.step (oracle/hk_oracle.c), {sec:.1f} s"}
 
 
+def reduce_over_ranks(elapsed, counters, dist, device):
+    """Whole-job numbers: the slowest rank's elapsed time (MAX) and the summed device counters (SUM).
+    The only collectives of the bench; none on the step path (arenas are sharded)."""
+    import torch
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor(counters, dtype=torch.int64, device=device)
+    dist.all_reduce(c)
+    return float(t.item()), c.cpu().numpy()
+
+
+def shard_offset(rank, n_per_rank):
+    """Global id of this rank's first arena: rank r owns [r*N, (r+1)*N); RNG streams key on the global id."""
+    return rank * n_per_rank
+
+
 def main():
     args = _args()
     import torch
@@ -83,7 +100,8 @@ def main():
 
     n = args.arenas
     pol = ("strong", "strong") if args.policy == "basic" else ("random", "random")
-    env = VecHockeyEnv(n, device=dev, policies=pol, auto_reset=True, seed=args.seed, arena_offset=rank * n)
+    env = VecHockeyEnv(n, device=dev, policies=pol, auto_reset=True, seed=args.seed,
+                       arena_offset=shard_offset(rank, n))
     env.reset()
     io = N.StepIO()
     io.obs = env.obs_buf.data_ptr()
@@ -115,12 +133,7 @@ def main():
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     cnt = env.counters()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor(cnt, dtype=torch.int64, device=dev)
-        dist.all_reduce(c)
-        cnt = c.cpu().numpy()
+        elapsed, cnt = reduce_over_ranks(elapsed, cnt, dist, dev)
     total_steps = n * world * args.steps
     assert int(cnt[N.CNT_STEPS]) == total_steps, (cnt, total_steps)
     assert int(cnt[N.CNT_OVERFLOW]) == 0, cnt

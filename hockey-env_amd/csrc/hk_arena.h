@@ -57,6 +57,9 @@ struct Arena {
   int keep_mode, max_t, time, done, winner, has1, has2, vel_ref;
   int force_big;  // diagnostics: always take the generic (large-island) solver
   int n_toi, overflow, n_big;  // TOI events, island overflow flag, large-island (generic) solves
+#ifdef HK_PHASE_TIMERS
+  int dg_vit_isl, dg_vit_toi, dg_pit, dg_toi_calls, dg_nc_max;  // diagnostics build: per-lane work
+#endif
   float *man;   // HBM manifolds
   float *ws;    // HBM slot workspace of large islands (HbmSlots)
   int64_t n, a;
@@ -447,7 +450,12 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt) {
     fslot_init_velocity(s, w);
   });
   S.each(nc, [&](FSlot &s, int) { fslot_warm_start(s, w.d); });
-  velocity_iterations(S, w.d, nc);
+  const int vit = velocity_iterations(S, w.d, nc);
+#ifdef HK_PHASE_TIMERS
+  w.dg_vit_isl += vit;
+  w.dg_nc_max = nc > w.dg_nc_max ? nc : w.dg_nc_max;
+#endif
+  (void)vit;
   S.each(nc, [&](FSlot &s, int) { fslot_store(s, w); });
 #pragma unroll
   for (int b = 0; b < 3; ++b)
@@ -465,6 +473,9 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt) {
         ms2 = isl == 2 ? fmin2(ms2, m) : ms2;
       }
     });
+#ifdef HK_PHASE_TIMERS
+    w.dg_pit++;
+#endif
     if (ms0 >= -3.0f * kLinearSlop) solved |= 1;
     if (ms1 >= -3.0f * kLinearSlop) solved |= 2;
     if (ms2 >= -3.0f * kLinearSlop) solved |= 4;
@@ -522,7 +533,11 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
   place(w.d.c0y, db, pick(w.d.cy, db, 0.0f));
   place(w.d.a0, db, pick(w.d.a, db, 0.0f));
   S.each(nc, [&](FSlot &s, int) { fslot_init_velocity(s, w); });
-  velocity_iterations(S, w.d, nc);
+  const int vit = velocity_iterations(S, w.d, nc);
+#ifdef HK_PHASE_TIMERS
+  w.dg_vit_toi += vit;
+#endif
+  (void)vit;
 #pragma unroll
   for (int b = 0; b < 3; ++b)
     if (b == db) integrate_one(sub_dt, w.d, b);
@@ -572,6 +587,9 @@ HK_DEV void solve_toi(Arena &w, float dt) {
           const Proxy pA = make_proxy(SC.fx[SC.pairA[p]]), pB = make_proxy(SC.fx[SC.pairB[p]]);
           float beta;
           const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);
+#ifdef HK_PHASE_TIMERS
+          w.dg_toi_calls++;
+#endif
           alpha = st == TOI_TOUCHING ? fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f) : 1.0f;
         }
         LDS(w, kLdsToi + p) = alpha;

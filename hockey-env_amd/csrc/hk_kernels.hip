@@ -56,6 +56,11 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
 #ifdef HK_PHASE_TIMERS
   if ((threadIdx.x & 63) == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(&s.counters[8 + k], T.acc[k]);
+  if (io.debug && live) {  // wave cycles (whole step) for the tail analysis
+    unsigned long long tot = 0;
+    for (int k = 0; k < 8; ++k) tot += T.acc[k];
+    io.debug[a * 8] = (float)tot;
+  }
 #endif
 }
 

@@ -414,12 +414,13 @@ template <> struct SlotCap<HbmSlots> { static constexpr int value = kBigC; };
 
 // 180 velocity iterations over nc slots, with the exact periodic early exit
 template <typename SL>
-HK_DEV void velocity_iterations(SL &S, Dyn &B, int nc) {
+HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
   uint32_t sb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) sb[k] = 0u;
   bool active = nc > 0;
-  for (int it = 0; it < kVelIters && active; ++it) {
+  int it = 0;
+  for (; it < kVelIters && active; ++it) {
     S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
     if ((it & 3) == 3) {
       uint32_t diff = 0u;
@@ -443,6 +444,7 @@ HK_DEV void velocity_iterations(SL &S, Dyn &B, int nc) {
       if (it >= 7 && diff == 0u) active = false;
     }
   }
+  return it;
 }
 
 HK_DEV void fslot_store(const FSlot &s, Arena &w) {

@@ -89,6 +89,9 @@ HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, in
   w.overflow = 0;
   w.n_big = 0;
   w.force_big = 0;
+#ifdef HK_PHASE_TIMERS
+  w.dg_vit_isl = w.dg_vit_toi = w.dg_pit = w.dg_toi_calls = w.dg_nc_max = 0;
+#endif
   w.touch = (uint32_t)I(s, I_TOUCH, a);
   w.enabled = (uint32_t)I(s, I_ENABLED, a);
   w.toiflag = w.cisl = w.bisl = 0u;
@@ -299,6 +302,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   HK_TIC(T, 0);
   presolve(w, a8);
   HK_TIC(T, 1);
+#ifndef HK_PHASE_TIMERS
   if (io.debug) {
 #ifdef HK_TRACE
     float *d = io.debug + a * kTraceStride;
@@ -309,6 +313,8 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     d[4] = w.d.fx[B_PK]; d[5] = w.d.fy[B_PK]; d[6] = w.d.tq[B_P1]; d[7] = w.d.tq[B_P2];
     d[8] = w.d.ld[B_P1]; d[9] = w.d.ld[B_P2]; d[10] = w.d.ld[B_PK]; d[11] = w.d.ad[B_P1]; d[12] = w.d.ad[B_P2];
   }
+#endif
+
   if (!(io.flags & 1)) {
     world_step(w, T);
   } else {
@@ -346,6 +352,13 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   out.ntoi = w.n_toi;
   out.ovf = w.overflow;
   out.nbig = w.n_big;
+#ifdef HK_PHASE_TIMERS
+  if (io.debug) {  // diagnostics build: per-lane work counters
+    float *d = io.debug + a * 8;
+    d[1] = (float)w.n_toi; d[2] = (float)w.dg_vit_isl; d[3] = (float)w.dg_vit_toi; d[4] = (float)w.dg_pit;
+    d[5] = (float)w.dg_toi_calls; d[6] = (float)w.dg_nc_max; d[7] = (float)w.n_big;
+  }
+#endif
 }
 
 

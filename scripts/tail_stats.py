@@ -1,0 +1,57 @@
+"""Tail analysis (diagnostics build libhockey_hip_timers.so): per-wave step cycles and the per-lane work that
+drives the slowest waves.  Usage: python scripts/tail_stats.py [arenas] [steps]"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("HK_LIB", os.path.join(ROOT, "hockey-env_amd", "hockey_amd", "_lib", "libhockey_hip_timers.so"))
+sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
+import torch  # noqa: E402
+
+from hockey_amd import _native as N  # noqa: E402
+from hockey_amd.vec_env import VecHockeyEnv  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+env = VecHockeyEnv(n, device="cuda:0", policies=("strong", "strong"), auto_reset=True, seed=1)
+env.reset()
+dbg = torch.zeros((n, 8), dtype=torch.float32, device="cuda:0")
+io = N.StepIO()
+io.obs = env.obs_buf.data_ptr()
+io.reward = env.reward_buf.data_ptr()
+io.done = env.done_buf.data_ptr()
+for _ in range(300):
+    env.step_raw(io)
+io.debug = dbg.data_ptr()
+names = ["wave_cyc", "ntoi", "vit_isl", "vit_toi", "pit", "toi_calls", "nc_max", "nbig"]
+rows = []
+for s in range(steps):
+    env.step_raw(io)
+    torch.cuda.synchronize()
+    d = dbg.cpu().numpy().copy()
+    rows.append(d)
+D = np.stack(rows)  # [steps, n, 8]
+wave = D[:, ::64, 0]  # [steps, waves]
+print(f"wave cycles per step: mean {wave.mean():.0f}  median {np.median(wave):.0f}  p99 {np.percentile(wave, 99):.0f}  "
+      f"max-per-step mean {wave.max(1).mean():.0f}")
+lanes = D.reshape(steps, n // 64, 64, 8)
+for q in (50, 90, 99):
+    print(f"per-lane p{q}:", {nm: float(np.percentile(D[:, :, k], q)) for k, nm in enumerate(names) if k})
+print("per-lane max:", {nm: float(D[:, :, k].max()) for k, nm in enumerate(names) if k})
+# slowest waves: max-lane stats
+flat = wave.reshape(-1)
+idx = np.argsort(flat)[-10:]
+for i in idx[::-1]:
+    st, wv = divmod(int(i), n // 64)
+    L = lanes[st, wv]
+    print(f"step {st} wave {wv} cycles {flat[i]:.0f} | lane max:",
+          {nm: float(L[:, k].max()) for k, nm in enumerate(names) if k},
+          "| lane sum ntoi", float(L[:, 1].sum()), "vit_isl sum", float(L[:, 2].sum()))
+# correlation of wave cycles with wave-max stats
+for k, nm in enumerate(names):
+    if k:
+        m = lanes[:, :, :, k].max(2).reshape(-1)
+        c = np.corrcoef(m, flat)[0, 1] if m.std() > 0 else 0
+        print(f"corr(wave cycles, wave-max {nm}) = {c:.2f}")

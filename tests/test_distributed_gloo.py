@@ -1,0 +1,63 @@
+"""World-size-2 rehearsal of the multi-GPU bench path on CPU (gloo): arenas shard by global id with no
+collective on the step path; the bench's only collectives (MAX of elapsed, SUM of counters) reduce
+correctly; and the two shards together are bit-identical to one process running all arenas (shard
+invariance of the per-arena Philox streams).  The per-arena step is the kernel source's host build
+(tests/hostcheck.py), so no GPU is needed."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+N_PER_RANK, STEPS = 96, 60
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), root]
+    import bench
+    from hostcheck import HostVec
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    env = HostVec(N_PER_RANK, policies=("strong", "strong"), auto_reset=True, seed=5,
+                  arena_offset=bench.shard_offset(rank, N_PER_RANK))
+    for _ in range(STEPS):
+        env.step(None)
+    st, aux = env.get_state()
+    c = env.counters().astype(np.int64)
+    elapsed, total = bench.reduce_over_ranks(1.0 + rank, c, dist, torch.device("cpu"))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), st=st, aux=aux, c=c, total=total, elapsed=elapsed)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_matches_single_process(tmp_path):
+    from hostcheck import HostVec, lib
+
+    lib()  # build the harness once, before the workers load it
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]
+    # bench reductions: MAX elapsed, SUM counters
+    assert float(r[0]["elapsed"]) == 2.0 and float(r[1]["elapsed"]) == 2.0
+    assert np.array_equal(r[0]["total"], r[0]["c"] + r[1]["c"])
+    assert int(r[0]["total"][0]) == 2 * N_PER_RANK * STEPS
+    # shard invariance: ranks 0+1 == one process over 2N arenas
+    one = HostVec(2 * N_PER_RANK, policies=("strong", "strong"), auto_reset=True, seed=5, arena_offset=0)
+    for _ in range(STEPS):
+        one.step(None)
+    st, aux = one.get_state()
+    assert np.array_equal(st, np.concatenate([r[0]["st"], r[1]["st"]]))
+    assert np.array_equal(aux, np.concatenate([r[0]["aux"], r[1]["aux"]]))
