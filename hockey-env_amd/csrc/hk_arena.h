@@ -544,7 +544,27 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
   sync_xf(w, db);
 }
 
-HK_DEV void solve_toi(Arena &w, float dt) {
+// b2TimeOfImpact of static-vs-dynamic pair p (per-lane p) -> alpha in the step's [alpha0, 1] frame
+HK_DEV float toi_pair(Arena &w, int p) {
+  const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const float alpha0 = pick(w.d.al0, bB, 0.0f);  // == max(alpha0 A, alpha0 B) after alignment
+  const Proxy pA = make_proxy(SC.fx[SC.pairA[p]]), pB = make_proxy(SC.fx[SC.pairB[p]]);
+  float beta;
+  const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);
+#ifdef HK_PHASE_TIMERS
+  w.dg_toi_calls++;
+#endif
+  return st == TOI_TOUCHING ? fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f) : 1.0f;
+}
+HK_DEV void toi_drain(Arena &w, uint32_t &pending) {
+  while (pending) {
+    const int p = __ffs(pending) - 1;
+    pending &= pending - 1u;
+    LDS(w, kLdsToi + p) = toi_pair(w, p);
+  }
+}
+
+HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
 #pragma unroll
   for (int b = 0; b < 3; ++b) w.d.al0[b] = 0.0f;
   for (int k = 0; k < 8; ++k) LDS(w, kLdsSal0 + k) = 0.0f;
@@ -556,45 +576,54 @@ HK_DEV void solve_toi(Arena &w, float dt) {
   w.cisl = 0u;
   w.bisl = 0u;
   for (;;) {
-    int minc = -1;
-    float minAlpha = 1.0f;
+    HK_TIC(T, 4);  // diagnostics: events / min selection -> "toi-events"
+    // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
+    //     far rejection.  Pairs that need a real b2TimeOfImpact are queued per lane.  During a step the
+    //     alignment only ever advances a STATIC body's alpha0 (TOI events come in non-decreasing alpha, and
+    //     only the moved body's pairs are re-evaluated, so a0(static) <= a0(dynamic) for them); the queued
+    //     TOIs therefore see exactly the sweeps the sequential scan would.  Should a dynamic body ever be
+    //     advanced here, its lane first drains its queue so the sequential order is kept regardless.
+    uint32_t elig = 0u, pending = 0u;
     for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
       const uint32_t bit = 1u << p;
       if (!(w.enabled & bit)) continue;
       if (LDS(w, kLdsCnt + p) > (float)kMaxSubSteps) continue;
-      float alpha = 1.0f;
       if (w.toiflag & bit) {
-        alpha = LDS(w, kLdsToi + p);
-      } else {
-        if (SC.sensor[p]) continue;
-        const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
-        if (bA < 3) continue;                 // dynamic-dynamic, non-bullet: no continuous collision
-        if (!pick(w.d.awake, bB, 0)) continue;  // static A is never active
-        float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
-        float alpha0 = a0A;
-        if (a0A < a0B) {
-          alpha0 = a0B;
-          LDS(w, kLdsSal0 + bA - 3) = a0B;  // static b2Sweep::Advance: only alpha0 moves
-        } else if (a0B < a0A) {
-          alpha0 = a0A;
-          Sweep s = body_sweep(w, bB);
-          sweep_advance(s, alpha0);
-          body_set_sweep(w, bB, s);
-        }
-        if (pair_far_toi(w, p)) {
-          alpha = 1.0f;
-        } else {
-          const Proxy pA = make_proxy(SC.fx[SC.pairA[p]]), pB = make_proxy(SC.fx[SC.pairB[p]]);
-          float beta;
-          const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);
-#ifdef HK_PHASE_TIMERS
-          w.dg_toi_calls++;
-#endif
-          alpha = st == TOI_TOUCHING ? fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f) : 1.0f;
-        }
-        LDS(w, kLdsToi + p) = alpha;
-        w.toiflag |= bit;
+        elig |= bit;
+        continue;
       }
+      if (SC.sensor[p]) continue;
+      const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+      if (bA < 3) continue;                   // dynamic-dynamic, non-bullet: no continuous collision
+      if (!pick(w.d.awake, bB, 0)) continue;  // static A is never active
+      elig |= bit;
+      w.toiflag |= bit;
+      const float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
+      if (a0A < a0B) {
+        LDS(w, kLdsSal0 + bA - 3) = a0B;  // static b2Sweep::Advance: only alpha0 moves
+      } else if (a0B < a0A) {
+        toi_drain(w, pending);  // keep the sequential order for this lane (see above)
+        Sweep sw = body_sweep(w, bB);
+        sweep_advance(sw, a0A);
+        body_set_sweep(w, bB, sw);
+      }
+      if (pair_far_toi(w, p)) {
+        LDS(w, kLdsToi + p) = 1.0f;
+      } else {
+        pending |= bit;
+      }
+    }
+    HK_TIC(T, 6);  // diagnostics: scan pass -> "toi-scan"
+    // (2) per-lane queue: every lane runs b2TimeOfImpact on its own next pair (lanes stay converged on
+    //     the same code instead of serialising over the union of the wave's pairs)
+    toi_drain(w, pending);
+    HK_TIC(T, 7);  // diagnostics: b2TimeOfImpact -> "toi-solve" slot
+    // (3) Box2D's minimum: first pair (in order) with the smallest alpha
+    int minc = -1;
+    float minAlpha = 1.0f;
+    for (int p = 0; p < NP; ++p) {
+      if (!((elig >> p) & 1u)) continue;
+      const float alpha = LDS(w, kLdsToi + p);
       if (alpha < minAlpha) { minc = p; minAlpha = alpha; }
     }
     if (minc < 0 || 1.0f - 10.0f * kFltEps < minAlpha) break;
@@ -678,7 +707,7 @@ HK_DEV void world_step(Arena &w, PhaseT &T) {
   }
   HK_TIC(T, 3);
   HK_TRACE_POINT(w, 1);
-  solve_toi(w, dt);
+  solve_toi(w, dt, T);
   HK_TIC(T, 4);
   HK_TRACE_POINT(w, 2);
 #pragma unroll
