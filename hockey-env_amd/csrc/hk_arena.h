@@ -104,15 +104,23 @@ HK_DEV void trace_point(const Arena &w, int k) {
 // ------------------------------------------------------------------------------------------------
 // runtime-id access to the register body file (3-way selects, static -> default)
 // ------------------------------------------------------------------------------------------------
+// Operands are read into locals first so clang emits straight-line selects (v_cndmask) instead of the
+// branch trees it generates for conditional operators over memory operands.
 template <typename T>
 HK_DEV T pick(const T (&x)[3], int b, T dflt) {
-  return b == 0 ? x[0] : (b == 1 ? x[1] : (b == 2 ? x[2] : dflt));
+  const T x0 = x[0], x1 = x[1], x2 = x[2];
+  T r = dflt;
+  r = (b == 2) ? x2 : r;
+  r = (b == 1) ? x1 : r;
+  r = (b == 0) ? x0 : r;
+  return r;
 }
 template <typename T>
 HK_DEV void place(T (&x)[3], int b, T v) {
-  x[0] = b == 0 ? v : x[0];
-  x[1] = b == 1 ? v : x[1];
-  x[2] = b == 2 ? v : x[2];
+  const T x0 = x[0], x1 = x[1], x2 = x[2];
+  x[0] = (b == 0) ? v : x0;
+  x[1] = (b == 1) ? v : x1;
+  x[2] = (b == 2) ? v : x2;
 }
 HK_DEV float &LDS(Arena &w, int k) { return w.lds[k * 64 + w.lane]; }
 HK_DEV float &MF(const Arena &w, int slot, int field) { return w.man[((int64_t)slot * NMF + field) * w.n + w.a]; }
