@@ -36,6 +36,7 @@ constexpr float kLinearSleepTol = 0.01f;
 constexpr float kAngularSleepTol = 2.0f / 180.0f * kPi;
 constexpr int kMaxSubSteps = 8;
 constexpr int kMaxPolyVerts = 8;
+constexpr int kStaticVerts = 4;  // every static fixture of the scene is a quad (build_scene checks)
 constexpr int kVelIters = 180;
 constexpr int kPosIters = 60;
 constexpr float kFltMax = 3.402823466e+38f;

@@ -169,15 +169,49 @@ HK_DEV void collide_polygons(Manifold &m, const Fixture &pA, xform xfA, const Fi
 // ------------------------------------------------------------------------------------------------
 // GJK distance + TOI (b2Distance.cpp, b2TimeOfImpact.cpp)
 // ------------------------------------------------------------------------------------------------
-struct Proxy { const float *vx, *vy; int count; float radius; };
-HK_DEV Proxy make_proxy(const Fixture &f) { Proxy p; p.vx = f.vx; p.vy = f.vy; p.count = f.count; p.radius = f.radius; return p; }
-HK_DEV v2 pv(const Proxy &p, int i) { return V(p.vx[i], p.vy[i]); }
-HK_DEV int proxy_support(const Proxy &p, v2 d) {
+// Register proxies: the fixture's vertices are copied into registers once per query (statics have <= 4
+// vertices, players 7, the puck 1), so GJK / TOI iterations run on registers instead of re-loading
+// vertices from memory with per-lane addresses.  Vertex fetch by index is a select chain.
+template <int N>
+struct Proxy {
+  float vx[N], vy[N];
+  int count;
+  float radius;
+};
+template <int N>
+HK_DEV Proxy<N> make_proxy(const Fixture &f) {
+  Proxy<N> p;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    p.vx[k] = f.vx[k];
+    p.vy[k] = f.vy[k];
+  }
+  p.count = f.count;
+  p.radius = f.radius;
+  return p;
+}
+template <int N>
+HK_DEV v2 pv(const Proxy<N> &p, int i) {
+  float x = p.vx[0], y = p.vy[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k) {
+    const float xk = p.vx[k], yk = p.vy[k];
+    x = (i == k) ? xk : x;
+    y = (i == k) ? yk : y;
+  }
+  return V(x, y);
+}
+// b2DistanceProxy::GetSupport: first vertex with the strictly largest projection
+template <int N>
+HK_DEV int proxy_support(const Proxy<N> &p, v2 d) {
   int best = 0;
-  float bv = dot(pv(p, 0), d);
-  for (int i = 1; i < p.count; ++i) {
-    float v = dot(pv(p, i), d);
-    if (v > bv) { best = i; bv = v; }
+  float bv = dot(V(p.vx[0], p.vy[0]), d);
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+    const float v = dot(V(p.vx[i], p.vy[i]), d);
+    const bool take = (i < p.count) && (v > bv);
+    best = take ? i : best;
+    bv = take ? v : bv;
   }
   return best;
 }
@@ -192,7 +226,8 @@ HK_DEV float simplex_metric(const Simplex &s) {
   if (s.count == 3) return crs(vsub(s.v2.w, s.v1.w), vsub(s.v3.w, s.v1.w));
   return 0.0f;
 }
-HK_DEV SVert make_svert(const Proxy &pA, xform xA, const Proxy &pB, xform xB, int iA, int iB) {
+template <typename PA, typename PB>
+HK_DEV SVert make_svert(const PA &pA, xform xA, const PB &pB, xform xB, int iA, int iB) {
   SVert v;
   v.iA = iA;
   v.iB = iB;
@@ -202,7 +237,8 @@ HK_DEV SVert make_svert(const Proxy &pA, xform xA, const Proxy &pB, xform xB, in
   v.a = 0.0f;
   return v;
 }
-HK_DEV void simplex_read(Simplex &s, const SimplexCache &cache, const Proxy &pA, xform xA, const Proxy &pB, xform xB) {
+template <typename PA, typename PB>
+HK_DEV void simplex_read(Simplex &s, const SimplexCache &cache, const PA &pA, xform xA, const PB &pB, xform xB) {
   s.count = cache.count;
   s.v1.wA = s.v1.wB = s.v1.w = V(0.0f, 0.0f);
   s.v1.a = 0.0f;
@@ -293,7 +329,8 @@ HK_DEV void solve3(Simplex &s) {
 }
 
 // b2Distance (returns the distance; witness points are not needed by the callers)
-HK_DEV float gjk_distance(SimplexCache &cache, const Proxy &pA, xform xA, const Proxy &pB, xform xB, int use_radii) {
+template <typename PA, typename PB>
+HK_DEV float gjk_distance(SimplexCache &cache, const PA &pA, xform xA, const PB &pB, xform xB, int use_radii) {
   Simplex s;
   simplex_read(s, cache, pA, xA, pB, xB);
   int sA0 = 0, sA1 = 0, sA2 = 0, sB0 = 0, sB1 = 0, sB2 = 0, saveCount;
@@ -337,7 +374,8 @@ HK_DEV float gjk_distance(SimplexCache &cache, const Proxy &pA, xform xA, const 
 }
 
 HK_DEV int test_overlap(const Fixture &fA, xform xA, const Fixture &fB, xform xB) {
-  Proxy pA = make_proxy(fA), pB = make_proxy(fB);
+  const Proxy<kStaticVerts> pA = make_proxy<kStaticVerts>(fA);  // A: a static goal sensor
+  const Proxy<kMaxPolyVerts> pB = make_proxy<kMaxPolyVerts>(fB);
   SimplexCache cache;
   cache.count = 0;
   cache.metric = 0.0f;
@@ -366,9 +404,17 @@ HK_DEV void sweep_normalize(Sweep &s) {
 }
 
 enum { SF_POINTS = 0, SF_FACEA, SF_FACEB };
-struct SepFn { Proxy pA, pB; Sweep sA, sB; int type; v2 lp, axis; };
+template <typename PA, typename PB>
+struct SepFn {
+  PA pA;
+  PB pB;
+  Sweep sA, sB;
+  int type;
+  v2 lp, axis;
+};
 
-HK_DEV void sep_init(SepFn &f, const SimplexCache &cache, const Proxy &pA, const Sweep &sA, const Proxy &pB,
+template <typename PA, typename PB>
+HK_DEV void sep_init(SepFn<PA, PB> &f, const SimplexCache &cache, const PA &pA, const Sweep &sA, const PB &pB,
                      const Sweep &sB, float t1) {
   f.pA = pA; f.pB = pB; f.sA = sA; f.sB = sB;
   xform xA, xB;
@@ -404,7 +450,8 @@ HK_DEV void sep_init(SepFn &f, const SimplexCache &cache, const Proxy &pA, const
     if (s < 0.0f) f.axis = vneg(f.axis);
   }
 }
-HK_DEV float sep_find_min(const SepFn &f, int &iA, int &iB, float t) {
+template <typename PA, typename PB>
+HK_DEV float sep_find_min(const SepFn<PA, PB> &f, int &iA, int &iB, float t) {
   xform xA, xB;
   sweep_xf(f.sA, xA, t);
   sweep_xf(f.sB, xB, t);
@@ -432,7 +479,8 @@ HK_DEV float sep_find_min(const SepFn &f, int &iA, int &iB, float t) {
     return dot(vsub(a, b), normal);
   }
 }
-HK_DEV float sep_eval(const SepFn &f, int iA, int iB, float t) {
+template <typename PA, typename PB>
+HK_DEV float sep_eval(const SepFn<PA, PB> &f, int iA, int iB, float t) {
   xform xA, xB;
   sweep_xf(f.sA, xA, t);
   sweep_xf(f.sB, xB, t);
@@ -454,7 +502,8 @@ HK_DEV float sep_eval(const SepFn &f, int iA, int iB, float t) {
 
 enum { TOI_UNKNOWN = 0, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
 
-HK_DEV int time_of_impact(const Proxy &pA, const Proxy &pB, Sweep sA, Sweep sB, float tMax, float &t_out) {
+template <typename PA, typename PB>
+HK_DEV int time_of_impact(const PA &pA, const PB &pB, Sweep sA, Sweep sB, float tMax, float &t_out) {
   int state = TOI_UNKNOWN;
   t_out = tMax;
   sweep_normalize(sA);
@@ -474,7 +523,7 @@ HK_DEV int time_of_impact(const Proxy &pA, const Proxy &pB, Sweep sA, Sweep sB, 
     float dist = gjk_distance(cache, pA, xA, pB, xB, 0);
     if (dist <= 0.0f) { state = TOI_OVERLAPPED; t_out = 0.0f; break; }
     if (dist < target + tol) { state = TOI_TOUCHING; t_out = t1; break; }
-    SepFn fcn;
+    SepFn<PA, PB> fcn;
     sep_init(fcn, cache, pA, sA, pB, sB, t1);
     int done = 0;
     float t2 = tMax;

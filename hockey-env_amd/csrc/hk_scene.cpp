@@ -214,6 +214,8 @@ void build_scene(Scene &sc) {
     sc.manslot[p] = sc.sensor[p] ? -1 : slot++;
     // the solver derives radii from this layout (hk_solver.h pair_rA / pair_rB)
     if (fA.radius != kPolyRadius || (fB.body != B_PK && fB.radius != kPolyRadius) || fA.body == B_PK) std::abort();
+    // TOI and sensor queries hold a static fixture A in a 4-vertex register proxy (hk_geom.h)
+    if (fA.body >= B_WT && fA.count > kStaticVerts) std::abort();
   }
   for (int f = 0; f < NF; ++f) {
     const Fixture &fx = sc.fx[f];
