@@ -35,6 +35,8 @@ def _args():
     ap.add_argument("--policy", choices=["basic", "random"], default="basic")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rollout", type=int, default=50,
+                    help="also time hk_rollout with this many steps per launch (0 = skip); reported under 'rollout'")
     ap.add_argument("--cpu-arenas", type=int, default=32768, help="CPU baseline sample: arenas x 250 steps")
     return ap.parse_args()
 
@@ -80,6 +82,38 @@ def reduce_over_ranks(elapsed, counters, dist, device):
 def shard_offset(rank, n_per_rank):
     """Global id of this rank's first arena: rank r owns [r*N, (r+1)*N); RNG streams key on the global id."""
     return rank * n_per_rank
+
+
+def _time_rollout(env, N, torch, dist, world, dev, args):
+    """Same workload through hk_rollout: K steps per launch, every step's obs/reward/done/info written
+    ([K, N, ...] buffers), so a launch is paced by the average wave instead of each step's slowest wave."""
+    k, n = args.rollout, env.n
+    launches = max(1, args.steps // k)
+    obs = torch.empty((k, n, N.OBS_DIM), dtype=torch.float32, device=dev)
+    rew = torch.empty((k, n), dtype=torch.float32, device=dev)
+    done = torch.empty((k, n), dtype=torch.uint8, device=dev)
+    info = torch.empty((k, n, N.INFO_DIM), dtype=torch.float32, device=dev)
+    io = N.StepIO()
+    io.obs, io.reward, io.done, io.info = obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr()
+    env.rollout_raw(k, io)  # warm
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        env.rollout_raw(k, io)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps = launches * k
+    return {"steps_per_launch": k, "launches": launches, "value": n * world * steps / elapsed,
+            "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3}
 
 
 def main():
@@ -134,6 +168,9 @@ def main():
     cnt = env.counters()
     if world > 1:
         elapsed, cnt = reduce_over_ranks(elapsed, cnt, dist, dev)
+    rollout = None
+    if args.rollout > 1:
+        rollout = _time_rollout(env, N, torch, dist, world, dev, args)
     total_steps = n * world * args.steps
     assert int(cnt[N.CNT_STEPS]) == total_steps, (cnt, total_steps)
     assert int(cnt[N.CNT_OVERFLOW]) == 0, cnt
@@ -167,6 +204,8 @@ def main():
             "episodes": int(cnt[N.CNT_EPISODES]),
             "toi_events": int(cnt[N.CNT_TOI]),
         }
+        if rollout is not None:
+            line["rollout"] = rollout
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas)
         print(json.dumps(line), flush=True)

@@ -397,7 +397,7 @@ namespace hk {
 // dynamic body), position early exit and sleep per island.
 // ------------------------------------------------------------------------------------------------
 template <typename SL>
-HK_DEV bool solve_islands(Arena &w, SL &S, float dt) {
+HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
   constexpr int MAXS = SlotCap<SL>::value;
   const float h = dt;
   int island_of[3] = {-1, -1, -1};
@@ -458,7 +458,9 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt) {
     fslot_init_velocity(s, w);
   });
   S.each(nc, [&](FSlot &s, int) { fslot_warm_start(s, w.d); });
+  HK_TIC(T, 2);  // diagnostics: island setup (DFS, integrate, constraint init, warm start)
   const int vit = velocity_iterations(S, w.d, nc);
+  HK_TIC(T, 3);  // diagnostics: velocity iterations
 #ifdef HK_PHASE_TIMERS
   w.dg_vit_isl += vit;
   w.dg_nc_max = nc > w.dg_nc_max ? nc : w.dg_nc_max;
@@ -585,7 +587,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
   w.cisl = 0u;
   w.bisl = 0u;
   for (;;) {
-    HK_TIC(T, 4);  // diagnostics: events / min selection -> "toi-events"
+    HK_TIC(T, 5);  // diagnostics: events / min selection -> "toi-events"
     // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
     //     far rejection.  Pairs that need a real b2TimeOfImpact are queued per lane.  During a step the
     //     alignment only ever advances a STATIC body's alpha0 (TOI events come in non-decreasing alpha, and
@@ -702,22 +704,22 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
 HK_DEV void world_step(Arena &w, PhaseT &T) {
   const float dt = 0.02f;
   collide(w);
-  HK_TIC(T, 2);
+  HK_TIC(T, 1);
   HK_TRACE_POINT(w, 0);
   bool done = false;
   if (!w.force_big) {
     RegSlots<kIslandC> S;
-    done = solve_islands(w, S, dt);
+    done = solve_islands(w, S, dt, T);
   }
   if (!done) {  // more island contacts than register slots: identical solve on the HBM slot file
     w.n_big++;
     HbmSlots S{w.ws, w.n, w.a};
-    solve_islands(w, S, dt);
+    solve_islands(w, S, dt, T);
   }
-  HK_TIC(T, 3);
+  HK_TIC(T, 4);  // diagnostics: position iterations + sleep
   HK_TRACE_POINT(w, 1);
   solve_toi(w, dt, T);
-  HK_TIC(T, 4);
+  HK_TIC(T, 5);
   HK_TRACE_POINT(w, 2);
 #pragma unroll
   for (int b = 0; b < 3; ++b) { w.d.fx[b] = 0.0f; w.d.fy[b] = 0.0f; w.d.tq[b] = 0.0f; }

@@ -161,11 +161,12 @@ int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t 
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_reset");
 }
 
-int hk_step(void *ctx, const hk_step_io *io, void *stream) {
-  if (!ctx || !io) return fail(HK_E_INVALID, "hk_step: NULL argument%s");
+static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int nsteps, void *stream) {
+  if (!ctx || !io) return fail(HK_E_INVALID, "%s: NULL argument", who);
+  if (nsteps < 1) return fail(HK_E_INVALID, "%s: n_steps must be >= 1", who);
   Ctx *c = (Ctx *)ctx;
   if (!io->actions && (c->cfg.policy[0] == HK_POLICY_EXTERNAL || c->cfg.policy[1] == HK_POLICY_EXTERNAL))
-    return fail(HK_E_INVALID, "hk_step: a player takes external actions but io->actions is NULL%s");
+    return fail(HK_E_INVALID, "%s: a player takes external actions but io->actions is NULL", who);
   hk::StepIO s;
   s.actions = io->actions;
   s.opp_inc = io->opp_inc;
@@ -180,8 +181,14 @@ int hk_step(void *ctx, const hk_step_io *io, void *stream) {
   s.debug = io->debug;
   s.flags = io->flags;
   DeviceGuard g(c->device);
-  hipError_t e = hk::launch_step(c->s, c->cfg, s, (hipStream_t)stream);
-  return e == hipSuccess ? HK_OK : hipfail(e, "hk_step");
+  hipError_t e = hk::launch_step(c->s, c->cfg, s, nsteps, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, who);
+}
+
+int hk_step(void *ctx, const hk_step_io *io, void *stream) { return launch_steps("hk_step", ctx, io, 1, stream); }
+
+int hk_rollout(void *ctx, int32_t n_steps, const hk_step_io *io, void *stream) {
+  return launch_steps("hk_rollout", ctx, io, n_steps, stream);
 }
 
 int hk_get_state(void *ctx, float *state, int32_t *aux, void *stream) {

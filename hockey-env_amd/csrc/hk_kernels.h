@@ -46,7 +46,7 @@ struct StepIO {
 hipError_t launch_init(const DevState &s, const KCfg &cfg, hipStream_t st);
 hipError_t launch_reset(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *params,
                         const int32_t *max_t, const uint8_t *one, hipStream_t st);
-hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, hipStream_t st);
+hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, int nsteps, hipStream_t st);
 hipError_t launch_observe(const DevState &s, const KCfg &cfg, float *obs, float *obs2, hipStream_t st);
 hipError_t launch_get_state(const DevState &s, const KCfg &cfg, float *state, int32_t *aux, hipStream_t st);
 hipError_t launch_set_state(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *state,

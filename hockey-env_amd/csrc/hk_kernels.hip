@@ -25,7 +25,30 @@ __global__ void __launch_bounds__(64) reset_kernel(DevState s, KCfg cfg, const u
   reset_lane(s, cfg, a, params, max_t_in, one_in);
 }
 
-__global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO io) {
+// io pointers of step k of a rollout: every array carries a leading [nsteps] dimension
+HK_DEV StepIO step_io(const StepIO &io, int k, int nsteps, int64_t n) {
+  StepIO r = io;
+  const int64_t o = (int64_t)k * n;
+  r.actions = io.actions ? io.actions + o * 8 : nullptr;
+  r.opp_inc = io.opp_inc ? io.opp_inc + o * 2 : nullptr;
+  r.obs = io.obs ? io.obs + o * 18 : nullptr;
+  r.obs2 = io.obs2 ? io.obs2 + o * 18 : nullptr;
+  r.reward = io.reward ? io.reward + o : nullptr;
+  r.reward2 = io.reward2 ? io.reward2 + o : nullptr;
+  r.done = io.done ? io.done + o : nullptr;
+  r.info = io.info ? io.info + o * 4 : nullptr;
+  r.info2 = io.info2 ? io.info2 + o * 4 : nullptr;
+  r.actions_out = io.actions_out ? io.actions_out + o * 8 : nullptr;
+  r.debug = (k == nsteps - 1) ? io.debug : nullptr;  // diagnostics describe the last step
+  return r;
+}
+
+// nsteps consecutive HockeyEnv.step calls of every arena (nsteps == 1: hk_step; > 1: hk_rollout).  The
+// arenas of a wave advance independently of every other wave, so a rollout launch is not paced by the
+// slowest wave of each step.
+template <bool kRollout>
+__global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO io, int nsteps) {
+  if (!kRollout) nsteps = 1;
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = a < s.n;
   int done_edge = 0, win1 = 0, win2 = 0, ntoi = 0, ovf = 0, nbig = 0;
@@ -36,27 +59,30 @@ __global__ void __launch_bounds__(64) step_kernel(DevState s, KCfg cfg, StepIO i
 #endif
   __shared__ float lds[kLdsPerLane * 64];
   if (live) {
-    LaneOut out;
-    step_lane(s, cfg, io, a, lds, threadIdx.x & 63, T, out);
-    done_edge = out.done_edge;
-    win1 = out.win1;
-    win2 = out.win2;
-    ntoi = out.ntoi;
-    ovf = out.ovf;
-    nbig = out.nbig;
+    for (int k = 0; k < nsteps; ++k) {
+      LaneOut out;
+      step_lane(s, cfg, step_io(io, k, nsteps, s.n), a, lds, threadIdx.x & 63, T, out);
+      done_edge += out.done_edge;
+      win1 += out.win1;
+      win2 += out.win2;
+      ntoi += out.ntoi;
+      ovf |= out.ovf;
+      nbig += out.nbig;
+    }
   }
-  wave_count(s.counters, 0, live);
-  wave_count(s.counters, 1, done_edge);
-  wave_count(s.counters, 2, win1);
-  wave_count(s.counters, 3, win2);
-  // few lanes carry TOI events / large islands; one atomic per lane that has any
+  const unsigned long long lanes = __ballot(live);
+  if ((threadIdx.x & 63) == 0 && lanes) atomicAdd(&s.counters[0], (unsigned long long)__popcll(lanes) * nsteps);
+  // per-lane sums (episode ends, goals, TOI events, large islands are sparse): one atomic per lane that has any
+  if (done_edge > 0) atomicAdd(&s.counters[1], (unsigned long long)done_edge);
+  if (win1 > 0) atomicAdd(&s.counters[2], (unsigned long long)win1);
+  if (win2 > 0) atomicAdd(&s.counters[3], (unsigned long long)win2);
   if (ntoi > 0) atomicAdd(&s.counters[4], (unsigned long long)ntoi);
   wave_count(s.counters, 5, ovf);
   if (nbig > 0) atomicAdd(&s.counters[6], (unsigned long long)nbig);
 #ifdef HK_PHASE_TIMERS
   if ((threadIdx.x & 63) == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(&s.counters[8 + k], T.acc[k]);
-  if (io.debug && live) {  // wave cycles (whole step) for the tail analysis
+  if (io.debug && live) {  // wave cycles (whole launch) for the tail analysis
     unsigned long long tot = 0;
     for (int k = 0; k < 8; ++k) tot += T.acc[k];
     io.debug[a * 8] = (float)tot;
@@ -104,8 +130,11 @@ hipError_t launch_reset(const DevState &s, const KCfg &cfg, const uint8_t *mask,
   hipLaunchKernelGGL(reset_kernel, grid_for(s.n), dim3(64), 0, st, s, cfg, mask, params, max_t, one);
   return hipGetLastError();
 }
-hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, hipStream_t st) {
-  hipLaunchKernelGGL(step_kernel, grid_for(s.n), dim3(64), 0, st, s, cfg, io);
+hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, int nsteps, hipStream_t st) {
+  if (nsteps == 1)
+    hipLaunchKernelGGL(step_kernel<false>, grid_for(s.n), dim3(64), 0, st, s, cfg, io, 1);
+  else
+    hipLaunchKernelGGL(step_kernel<true>, grid_for(s.n), dim3(64), 0, st, s, cfg, io, nsteps);
   return hipGetLastError();
 }
 hipError_t launch_observe(const DevState &s, const KCfg &cfg, float *obs, float *obs2, hipStream_t st) {

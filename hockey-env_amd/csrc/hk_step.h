@@ -301,7 +301,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   const int was_done = w.done;
   HK_TIC(T, 0);
   presolve(w, a8);
-  HK_TIC(T, 1);
+  HK_TIC(T, 0);
 #ifndef HK_PHASE_TIMERS
   if (io.debug) {
 #ifdef HK_TRACE

@@ -37,7 +37,7 @@ class StepIO(ctypes.Structure):
 
 
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",
-           "hk_step", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_observe", "hk_counters",
+           "hk_step", "hk_rollout", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_observe", "hk_counters",
            "hk_reset_counters",
            "hk_bytes_per_step"]
 
@@ -72,6 +72,7 @@ def lib():
     L.hk_set_policy.argtypes = [vp, i32, i32]
     L.hk_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hk_step.argtypes = [vp, ctypes.POINTER(StepIO), vp]
+    L.hk_rollout.argtypes = [vp, i32, ctypes.POINTER(StepIO), vp]
     L.hk_get_state.argtypes = [vp, vp, vp, vp]
     L.hk_set_state.argtypes = [vp, vp, vp, vp, vp]
     L.hk_observe.argtypes = [vp, vp, vp, vp]
@@ -79,7 +80,8 @@ def lib():
     L.hk_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), vp]
     L.hk_reset_counters.argtypes = [vp, vp]
     L.hk_bytes_per_step.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
-    for name in ["hk_create", "hk_destroy", "hk_set_policy", "hk_reset", "hk_step", "hk_get_state", "hk_set_state",
+    for name in ["hk_create", "hk_destroy", "hk_set_policy", "hk_reset", "hk_step", "hk_rollout", "hk_get_state",
+                 "hk_set_state",
                  "hk_observe", "hk_opponent_phase", "hk_counters", "hk_reset_counters", "hk_bytes_per_step"]:
         getattr(L, name).restype = i32
     _lib = L

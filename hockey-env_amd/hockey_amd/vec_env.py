@@ -183,6 +183,41 @@ class VecHockeyEnv:
         """Launch one step with a prepared StepIO (no Python-side allocation; for benchmarks)."""
         N.check(self.L.hk_step(self._ctx, ctypes.byref(io), self._stream()), "hk_step")
 
+    def rollout(self, n_steps, actions=None, with_agent_two=False, record_actions=False):
+        """``n_steps`` consecutive steps in one launch (hk_rollout).  Returns a StepResult whose tensors carry a
+        leading [n_steps] dimension.  ``actions`` ([n_steps, N, 8]) is needed only for external players."""
+        k, n = int(n_steps), self.n
+        d = self.device
+        a = None
+        if actions is not None:
+            a = torch.as_tensor(actions, dtype=torch.float32, device=d)
+            if a.shape != (k, n, N.ACT_DIM):
+                raise ValueError(f"actions must have shape ({k}, {n}, {N.ACT_DIM}), got {tuple(a.shape)}")
+            a = a.contiguous()
+        obs = torch.empty((k, n, N.OBS_DIM), dtype=torch.float32, device=d)
+        rew = torch.empty((k, n), dtype=torch.float32, device=d)
+        done = torch.empty((k, n), dtype=torch.uint8, device=d)
+        info = torch.empty((k, n, N.INFO_DIM), dtype=torch.float32, device=d)
+        io = N.StepIO()
+        io.actions = None if a is None else a.data_ptr()
+        io.obs, io.reward, io.done, io.info = obs.data_ptr(), rew.data_ptr(), done.data_ptr(), info.data_ptr()
+        obs2 = rew2 = info2 = acts = None
+        if with_agent_two:
+            obs2 = torch.empty_like(obs)
+            rew2 = torch.empty_like(rew)
+            info2 = torch.empty_like(info)
+            io.obs2, io.reward2, io.info2 = obs2.data_ptr(), rew2.data_ptr(), info2.data_ptr()
+        if record_actions:
+            acts = torch.empty((k, n, N.ACT_DIM), dtype=torch.float32, device=d)
+            io.actions_out = acts.data_ptr()
+        N.check(self.L.hk_rollout(self._ctx, k, ctypes.byref(io), self._stream()), "hk_rollout")
+        return StepResult(obs=obs, reward=rew, done=done, info=info, obs2=obs2, reward2=rew2, info2=info2,
+                          actions=acts)
+
+    def rollout_raw(self, n_steps, io):
+        """hk_rollout with a prepared StepIO whose arrays have a leading [n_steps] dimension."""
+        N.check(self.L.hk_rollout(self._ctx, int(n_steps), ctypes.byref(io), self._stream()), "hk_rollout")
+
     # ------------------------------------------------------------------ state / obs
     def observe(self):
         N.check(self.L.hk_observe(self._ctx, N.ptr(self.obs_buf), N.ptr(self.obs2_buf), self._stream()), "hk_observe")

@@ -112,6 +112,12 @@ int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t 
 
 int hk_step(void *ctx, const hk_step_io *io, void *stream);
 
+/* n_steps consecutive hk_step calls in ONE launch (a rollout with fused or pre-supplied actions).  Every
+ * io array gains a leading [n_steps] dimension (actions [n_steps,N,8], obs [n_steps,N,18], ...); debug, if
+ * given, describes the last step.  Results are bit-identical to n_steps hk_step calls; the waves of the
+ * launch advance independently instead of meeting at a per-step kernel boundary. */
+int hk_rollout(void *ctx, int32_t n_steps, const hk_step_io *io, void *stream);
+
 /* Raw state access: state [N,18] f32 (body origins / angles / velocities), aux [N,5] i32.
  * hk_set_state applies pybox2d setter semantics (SetTransform, SetLinearVelocity wakes, ...). */
 int hk_get_state(void *ctx, float *state, int32_t *aux, void *stream);

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from hockey_amd import _native as N  # noqa: E402
 from hockey_amd.vec_env import VecHockeyEnv  # noqa: E402
 
-NAMES = ["load+policy", "presolve", "collide", "islands", "toi-events", "outputs+store", "toi-scan", "toi-b2TOI"]
+NAMES = ["load+policy+presolve", "collide", "isl-setup", "isl-velocity", "isl-position+sleep", "toi-events+out", "toi-scan", "toi-b2TOI"]
 
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536

@@ -238,3 +238,29 @@ def test_facades_drop_in(golden):
     assert np.isfinite(obs).all()
     with pytest.raises(TypeError):
         env.reset(mode=1)  # reference quirk
+
+
+@pytest.mark.gpu
+def test_rollout_equals_repeated_steps():
+    """hk_rollout(K) == K hk_step calls, bit for bit: per-step outputs, final state and counters
+    (fused opponents + auto-reset, and external actions)."""
+    import torch
+
+    n, k = 512, 37
+    for pol in (("strong", "weak"), ("external", "strong")):
+        a = _vec(n, policies=pol, auto_reset=True, seed=11)
+        b = _vec(n, policies=pol, auto_reset=True, seed=11)
+        acts = None
+        if pol[0] == "external":
+            acts = torch.rand((k, n, 8), device="cuda:0") * 2 - 1
+        ro = a.rollout(k, actions=acts, with_agent_two=True, record_actions=True)
+        for t in range(k):
+            r = b.step(None if acts is None else acts[t], with_agent_two=True, record_actions=True)
+            for name in ("obs", "reward", "done", "info", "obs2", "reward2", "info2", "actions"):
+                assert torch.equal(getattr(ro, name)[t], getattr(r, name)), (pol, t, name)
+        sa, xa = a.get_state()
+        sb, xb = b.get_state()
+        assert torch.equal(sa, sb) and torch.equal(xa, xb)
+        assert np.array_equal(a.counters()[:7], b.counters()[:7])
+        a.close()
+        b.close()
