@@ -472,12 +472,13 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
     if (island_of[b] >= 0) integrate_one(h, w.d, b);
   int solved = 0;
   const int all = (1 << nisl) - 1;
+  S.load_geo(nc, w);
   for (int it = 0; it < kPosIters && (solved & all) != all; ++it) {
     float ms0 = 0.0f, ms1 = 0.0f, ms2 = 0.0f;
-    S.each(nc, [&](FSlot &s, int) {
+    S.each(nc, [&](FSlot &s, int i) {
       const int isl = fs_isl(s);
       if (!((solved >> isl) & 1)) {
-        const float m = fslot_solve_position(s, w, kBaumgarte, 0.0f);
+        const float m = fslot_solve_position(s, w, kBaumgarte, 0.0f, S.geo(i, s, w));
         ms0 = isl == 0 ? fmin2(ms0, m) : ms0;
         ms1 = isl == 1 ? fmin2(ms1, m) : ms1;
         ms2 = isl == 2 ? fmin2(ms2, m) : ms2;
@@ -533,8 +534,10 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
   });
   for (int it = 0; it < 20; ++it) {
     float minSep = 0.0f;
-    S.each(nc, [&](FSlot &s, int) {
-      minSep = fslot_solve_position(s, w, kToiBaumgarte, minSep);
+    S.each(nc, [&](FSlot &s, int i) {
+      // geometry re-read per pass here: caching it in the slot file miscompiles on gfx950 in this loop
+      // (ROCm 7.2; caught by the GPU lockstep tests), and TOI position passes are few
+      minSep = fslot_solve_position(s, w, kToiBaumgarte, minSep, man_geo(w, fs_pair(s)));
     });
     if (minSep >= -1.5f * kLinearSlop) break;
   }

@@ -303,11 +303,10 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
 
 // one NGS position pass over one contact (b2ContactSolver::SolvePositionConstraints body).  In this scene
 // SolveTOIPositionConstraints' mass gating is the identity (see solve_toi), so one routine serves both.
-HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float minSep) {
+HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float minSep, const ManGeo &m) {
   Dyn &B = w.d;
   const float mA = s.mA, mB = s.mB, iA = s.iA, iB = s.iB;
   const int bA = fs_bA(s), bB = fs_bB(s), pcount = fs_pcount(s);
-  const ManGeo m = man_geo(w, fs_pair(s));
   const v2 lcA = local_center(bA), lcB = local_center(bB);
   const float rAr = pair_rA(), rBr = pair_rB(bB);
   v2 cA, cB;
@@ -375,6 +374,13 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
 template <int C>
 struct RegSlots {
   FSlot s[C];
+  ManGeo g[C];  // position-phase geometry, loaded once per position loop (load_geo)
+  HK_DEV void load_geo(int nc, const Arena &w) {
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      if (i < nc) g[i] = man_geo(w, fs_pair(s[i]));
+  }
+  HK_DEV const ManGeo &geo(int i, const FSlot &, const Arena &) const { return g[i]; }
   template <typename Fn>
   HK_DEV void each(int nc, Fn &&fn) {
 #pragma unroll
@@ -407,6 +413,8 @@ struct HbmSlots {
   HK_DEV void set_pair(int nc, int p, int isl) {
     if (nc < kBigC) word(nc, (int)(offsetof(FSlot, bits) / 4)) = __int_as_float(p | (isl << 5));
   }
+  HK_DEV void load_geo(int, const Arena &) {}
+  HK_DEV ManGeo geo(int, const FSlot &s, const Arena &w) const { return man_geo(w, fs_pair(s)); }
 };
 template <typename SL> struct SlotCap;
 template <int C> struct SlotCap<RegSlots<C>> { static constexpr int value = C; };

@@ -1,8 +1,6 @@
 set -euo pipefail
-L=hockey-env_amd/hockey_amd/_lib
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-tail -1 gpurun_out/pytest_gpu.log
-for lib in libhockey_hip.so libhockey_hip_noslp.so; do
-  HK_LIB=$L/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 300 --warmup 200 > gpurun_out/bench_$lib.log 2>&1
-  echo "$lib $(grep -o '"value": [0-9.e+]*' gpurun_out/bench_$lib.log)"
+export HK_TRACE=1 HKH_LIB=hockey-env_amd/hockey_amd/_lib/libhockey_hostcheck_trace.so
+for v in A B; do
+  HK_LIB=hockey-env_amd/hockey_amd/_lib/libhockey_hip_trace_$v.so timeout -k 10 200 python scripts/debug_lockstep.py 0 1 1024 300 strong > gpurun_out/dbg_$v.log 2>&1
+  echo "$v: $(grep -E '^step|no div' gpurun_out/dbg_$v.log | head -2 | tr '\n' ' ')"
 done
