@@ -309,23 +309,29 @@ HK_DEV void begin_contact(Arena &w, int p) {
   }
 }
 
-HK_DEV void pair_update(Arena &w, int p) {
+// b2Contact::Update for a pair the broad phase could not reject: narrow phase, impulse carry-over,
+// wake-ups and BeginContact.
+HK_DEV void pair_update_near(Arena &w, int p) {
   const int fA = SC.pairA[p], fB = SC.pairB[p], bA = SC.pbodyA[p], bB = SC.pbodyB[p];
   const uint32_t bit = 1u << p;
   const int was = (w.touch & bit) != 0u;
   w.enabled |= bit;
   int touching;
-  if (pair_far_collide(w, p)) {
-    touching = 0;
-    if (!SC.sensor[p] && was) { set_awake(w, bA, 1); set_awake(w, bB, 1); }
-  } else {
+  {
     const xform xA = body_xf(w, bA), xB = body_xf(w, bB);
     if (SC.sensor[p]) {
       touching = test_overlap(SC.fx[fA], xA, SC.fx[fB], xB);
     } else {
       Manifold m;
-      if (SC.fx[fB].circle) collide_poly_circle(m, SC.fx[fA], xA, SC.fx[fB], xB);
-      else collide_polygons(m, SC.fx[fA], xA, SC.fx[fB], xB);
+      if (SC.fx[fB].circle) {  // puck: A is a static quad or a player
+        const RFix<1> cB = load_fix<1>(SC.fx[fB]);
+        if (bA >= 3) collide_poly_circle(m, load_fix<kStaticVerts>(SC.fx[fA]), xA, cB, xB);
+        else collide_poly_circle(m, load_fix<kMaxPolyVerts>(SC.fx[fA]), xA, cB, xB);
+      } else {  // player B: A is a static quad or the other player
+        const RFix<kMaxPolyVerts> pB = load_fix<kMaxPolyVerts>(SC.fx[fB]);
+        if (bA >= 3) collide_polygons(m, load_fix<kStaticVerts>(SC.fx[fA]), xA, pB, xB);
+        else collide_polygons(m, load_fix<kMaxPolyVerts>(SC.fx[fA]), xA, pB, xB);
+      }
       touching = m.count > 0;
       if (touching) {
         const int slot = SC.manslot[p];
@@ -375,8 +381,39 @@ HK_DEV void pair_update(Arena &w, int p) {
   if (!was && touching) begin_contact(w, p);
 }
 
-// b2ContactManager::Collide
+// b2Contact::Update for a pair the broad phase rejects: not touching (no manifold, no BeginContact)
+HK_DEV void pair_update_far(Arena &w, int p) {
+  const uint32_t bit = 1u << p;
+  const int was = (w.touch & bit) != 0u;
+  w.enabled |= bit;
+  if (!SC.sensor[p] && was) { set_awake(w, SC.pbodyA[p], 1); set_awake(w, SC.pbodyB[p], 1); }
+  w.touch &= ~bit;
+}
+
+HK_DEV void pair_update(Arena &w, int p) {
+  if (pair_far_collide(w, p)) pair_update_far(w, p);
+  else pair_update_near(w, p);
+}
+
+// b2ContactManager::Collide.  With every dynamic body awake (the normal state of play: no arena-step of a
+// strong-vs-strong run has a sleeping body) the pair order only matters among pairs that can touch
+// (wake-ups are no-ops, far pairs fire no BeginContact), so the narrow phases are run from a per-lane
+// queue: every lane works through its own near pairs in order instead of the wave serialising over the
+// union of all lanes' near pairs.  A lane with a sleeping body takes Box2D's sequential loop.
 HK_DEV void collide(Arena &w) {
+  if (w.d.awake[0] && w.d.awake[1] && w.d.awake[2]) {
+    uint32_t near = 0u;
+    for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
+      if (pair_far_collide(w, p)) pair_update_far(w, p);
+      else near |= 1u << p;
+    }
+    while (near) {
+      const int p = __ffs(near) - 1;
+      near &= near - 1u;
+      pair_update_near(w, p);
+    }
+    return;
+  }
   for (int p = 0; p < NP; ++p) {
     const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
     const int activeA = bA < 3 && pick(w.d.awake, bA, 0);

@@ -18,26 +18,79 @@ struct Manifold {
 };
 
 // ------------------------------------------------------------------------------------------------
-#define FXV(f, i) V((f).vx[i], (f).vy[i])
-#define FXN(f, i) V((f).nx[i], (f).ny[i])
+// Register fixtures.  A query copies the fixture's vertices / normals into registers once; loops run over
+// the compile-time bound N with `i < count` guards (statics have 4 vertices, players 7, the puck circle 1),
+// and a runtime index selects through a chain.  Whether the fixture address is wave-uniform (scalar loads)
+// or per lane (a lane's own pair), nothing is re-loaded inside the loops.
+// ------------------------------------------------------------------------------------------------
+template <int N>
+struct RFix {
+  float vx[N], vy[N], nx[N], ny[N];
+  int count;
+  float radius;
+};
+template <int N>
+HK_DEV RFix<N> load_fix(const Fixture &f) {
+  RFix<N> r;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    r.vx[k] = f.vx[k];
+    r.vy[k] = f.vy[k];
+    r.nx[k] = f.nx[k];
+    r.ny[k] = f.ny[k];
+  }
+  r.count = f.count;
+  r.radius = f.radius;
+  return r;
+}
+template <int N>
+HK_DEV v2 fxv(const RFix<N> &f, int i) {
+  float x = f.vx[0], y = f.vy[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k) {
+    const float xk = f.vx[k], yk = f.vy[k];
+    x = (i == k) ? xk : x;
+    y = (i == k) ? yk : y;
+  }
+  return V(x, y);
+}
+template <int N>
+HK_DEV v2 fxn(const RFix<N> &f, int i) {
+  float x = f.nx[0], y = f.ny[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k) {
+    const float xk = f.nx[k], yk = f.ny[k];
+    x = (i == k) ? xk : x;
+    y = (i == k) ? yk : y;
+  }
+  return V(x, y);
+}
 
-HK_DEV void collide_poly_circle(Manifold &m, const Fixture &pa, xform xfA, const Fixture &cb, xform xfB) {
+// b2CollidePolygonAndCircle (the circle's centre is its local position cb.vx[0], cb.vy[0])
+template <int NA>
+HK_DEV void collide_poly_circle(Manifold &m, const RFix<NA> &pa, xform xfA, const RFix<1> &cb, xform xfB) {
   m.count = 0;
-  v2 c = mul_xv(xfB, FXV(cb, 0));
+  const v2 cpos = V(cb.vx[0], cb.vy[0]);
+  v2 c = mul_xv(xfB, cpos);
   v2 cl = mulT_xv(xfA, c);
   int ni = 0;
   float sep = -kFltMax;
   float radius = pa.radius + cb.radius;
-  for (int i = 0; i < pa.count; ++i) {
-    float s = dot(FXN(pa, i), vsub(cl, FXV(pa, i)));
-    if (s > radius) return;
-    if (s > sep) { sep = s; ni = i; }
+  bool out = false;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    if (i < pa.count && !out) {
+      const float s = dot(V(pa.nx[i], pa.ny[i]), vsub(cl, V(pa.vx[i], pa.vy[i])));
+      if (s > radius) out = true;
+      else if (s > sep) { sep = s; ni = i; }
+    }
   }
+  if (out) return;
   int i1 = ni, i2 = i1 + 1 < pa.count ? i1 + 1 : 0;
-  v2 v1 = FXV(pa, i1), v2_ = FXV(pa, i2);
+  v2 v1 = fxv(pa, i1), v2_ = fxv(pa, i2);
   if (sep < kFltEps) {
-    m.count = 1; m.type = 1; m.ln = FXN(pa, ni); m.lp = vs(0.5f, vadd(v1, v2_));
-    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+    m.count = 1; m.type = 1; m.ln = fxn(pa, ni); m.lp = vs(0.5f, vadd(v1, v2_));
+    m.pt_lp[0] = cpos; m.id[0] = 0;
     return;
   }
   float u1 = dot(vsub(cl, v1), vsub(v2_, v1));
@@ -45,33 +98,44 @@ HK_DEV void collide_poly_circle(Manifold &m, const Fixture &pa, xform xfA, const
   if (u1 <= 0.0f) {
     if (vdist2(cl, v1) > radius * radius) return;
     m.count = 1; m.type = 1; m.ln = vsub(cl, v1); vnormalize(m.ln); m.lp = v1;
-    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+    m.pt_lp[0] = cpos; m.id[0] = 0;
   } else if (u2 <= 0.0f) {
     if (vdist2(cl, v2_) > radius * radius) return;
     m.count = 1; m.type = 1; m.ln = vsub(cl, v2_); vnormalize(m.ln); m.lp = v2_;
-    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+    m.pt_lp[0] = cpos; m.id[0] = 0;
   } else {
     v2 fc = vs(0.5f, vadd(v1, v2_));
-    float s = dot(vsub(cl, fc), FXN(pa, i1));
+    v2 n1 = fxn(pa, i1);
+    float s = dot(vsub(cl, fc), n1);
     if (s > radius) return;
-    m.count = 1; m.type = 1; m.ln = FXN(pa, i1); m.lp = fc;
-    m.pt_lp[0] = FXV(cb, 0); m.id[0] = 0;
+    m.count = 1; m.type = 1; m.ln = n1; m.lp = fc;
+    m.pt_lp[0] = cpos; m.id[0] = 0;
   }
 }
 
-HK_DEV float find_max_separation(int &edge, const Fixture &p1, xform xf1, const Fixture &p2, xform xf2) {
+// b2FindMaxSeparation (first edge with the strictly largest separation)
+template <int N1, int N2>
+HK_DEV float find_max_separation(int &edge, const RFix<N1> &p1, xform xf1, const RFix<N2> &p2, xform xf2) {
   xform xf = mulT_xx(xf2, xf1);
   int best = 0;
   float maxs = -kFltMax;
-  for (int i = 0; i < p1.count; ++i) {
-    v2 n = mul_rv(xf.q, FXN(p1, i));
-    v2 v1 = mul_xv(xf, FXV(p1, i));
-    float si = kFltMax;
-    for (int j = 0; j < p2.count; ++j) {
-      float sij = dot(n, vsub(FXV(p2, j), v1));
-      if (sij < si) si = sij;
+#pragma unroll
+  for (int i = 0; i < N1; ++i) {
+    if (i < p1.count) {
+      v2 n = mul_rv(xf.q, V(p1.nx[i], p1.ny[i]));
+      v2 v1 = mul_xv(xf, V(p1.vx[i], p1.vy[i]));
+      float si = kFltMax;
+#pragma unroll
+      for (int j = 0; j < N2; ++j) {
+        if (j < p2.count) {
+          const float sij = dot(n, vsub(V(p2.vx[j], p2.vy[j]), v1));
+          si = sij < si ? sij : si;
+        }
+      }
+      const bool take = si > maxs;
+      maxs = take ? si : maxs;
+      best = take ? i : best;
     }
-    if (si > maxs) { maxs = si; best = i; }
   }
   edge = best;
   return maxs;
@@ -80,18 +144,24 @@ HK_DEV float find_max_separation(int &edge, const Fixture &p1, xform xf1, const 
 struct ClipV { v2 v; uint32_t id; };
 HK_DEV uint32_t cf_id(uint32_t ia, uint32_t ib, uint32_t ta, uint32_t tb) { return ia | (ib << 8) | (ta << 16) | (tb << 24); }
 
-HK_DEV void find_incident_edge(ClipV c[2], const Fixture &p1, xform xf1, int edge1, const Fixture &p2, xform xf2) {
-  v2 n1 = mulT_rv(xf2.q, mul_rv(xf1.q, FXN(p1, edge1)));
+template <int N1, int N2>
+HK_DEV void find_incident_edge(ClipV c[2], const RFix<N1> &p1, xform xf1, int edge1, const RFix<N2> &p2, xform xf2) {
+  v2 n1 = mulT_rv(xf2.q, mul_rv(xf1.q, fxn(p1, edge1)));
   int index = 0;
   float mind = kFltMax;
-  for (int i = 0; i < p2.count; ++i) {
-    float d = dot(n1, FXN(p2, i));
-    if (d < mind) { mind = d; index = i; }
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    if (i < p2.count) {
+      const float d = dot(n1, V(p2.nx[i], p2.ny[i]));
+      const bool take = d < mind;
+      mind = take ? d : mind;
+      index = take ? i : index;
+    }
   }
   int i1 = index, i2 = i1 + 1 < p2.count ? i1 + 1 : 0;
-  c[0].v = mul_xv(xf2, FXV(p2, i1));
+  c[0].v = mul_xv(xf2, fxv(p2, i1));
   c[0].id = cf_id(edge1, i1, 1, 0);
-  c[1].v = mul_xv(xf2, FXV(p2, i2));
+  c[1].v = mul_xv(xf2, fxv(p2, i2));
   c[1].id = cf_id(edge1, i2, 1, 0);
 }
 
@@ -109,25 +179,15 @@ HK_DEV int clip_segment(ClipV out[2], const ClipV in[2], v2 normal, float offset
   return (int)k0 + (int)k1 + (int)cross;
 }
 
-HK_DEV void collide_polygons(Manifold &m, const Fixture &pA, xform xfA, const Fixture &pB, xform xfB) {
-  m.count = 0;
-  float total = pA.radius + pB.radius;
-  int eA = 0, eB = 0;
-  float sA = find_max_separation(eA, pA, xfA, pB, xfB);
-  if (sA > total) return;
-  float sB = find_max_separation(eB, pB, xfB, pA, xfA);
-  if (sB > total) return;
-  const float k_tol = 0.1f * kLinearSlop;
-  const bool flip = sB > sA + k_tol;
-  const Fixture &p1 = flip ? pB : pA;
-  const Fixture &p2 = flip ? pA : pB;
-  xform xf1 = flip ? xfB : xfA, xf2 = flip ? xfA : xfB;
-  int edge1 = flip ? eB : eA;
+// the reference-face part of b2CollidePolygons (p1 = reference polygon, p2 = incident polygon)
+template <int N1, int N2>
+HK_DEV void clip_polygons(Manifold &m, const RFix<N1> &p1, xform xf1, int edge1, const RFix<N2> &p2, xform xf2,
+                          bool flip, float total) {
   m.type = flip ? 2 : 1;
   ClipV inc[2];
   find_incident_edge(inc, p1, xf1, edge1, p2, xf2);
   int iv1 = edge1, iv2 = edge1 + 1 < p1.count ? edge1 + 1 : 0;
-  v2 v11 = FXV(p1, iv1), v12 = FXV(p1, iv2);
+  v2 v11 = fxv(p1, iv1), v12 = fxv(p1, iv2);
   v2 lt = vsub(v12, v11);
   vnormalize(lt);
   v2 ln = crs_vs(lt, 1.0f);
@@ -164,6 +224,21 @@ HK_DEV void collide_polygons(Manifold &m, const Fixture &pA, xform xfA, const Fi
   m.pt_lp[1] = q[1];
   m.id[1] = qid[1];
   m.count = (int)keep[0] + (int)keep[1];
+}
+
+// b2CollidePolygons
+template <int NA, int NB>
+HK_DEV void collide_polygons(Manifold &m, const RFix<NA> &pA, xform xfA, const RFix<NB> &pB, xform xfB) {
+  m.count = 0;
+  float total = pA.radius + pB.radius;
+  int eA = 0, eB = 0;
+  float sA = find_max_separation(eA, pA, xfA, pB, xfB);
+  if (sA > total) return;
+  float sB = find_max_separation(eB, pB, xfB, pA, xfA);
+  if (sB > total) return;
+  const float k_tol = 0.1f * kLinearSlop;
+  if (sB > sA + k_tol) clip_polygons(m, pB, xfB, eB, pA, xfA, true, total);
+  else clip_polygons(m, pA, xfA, eA, pB, xfB, false, total);
 }
 
 // ------------------------------------------------------------------------------------------------

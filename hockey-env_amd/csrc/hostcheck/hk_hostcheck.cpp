@@ -126,6 +126,13 @@ void hkh_observe(void *h, float *obs, float *obs2) {
   for (int64_t a = 0; a < c->n; ++a) observe_lane(c->s, c->cfg, a, obs, obs2);
 }
 
+// raw SoA state (diagnostics): f [NFF][N] floats, i [NIF][N] ints
+void hkh_raw(void *h, float **f, int32_t **i) {
+  HostCtx *c = (HostCtx *)h;
+  *f = c->f.data();
+  *i = c->i.data();
+}
+
 void hkh_counters(void *h, unsigned long long *out16) {
   HostCtx *c = (HostCtx *)h;
   std::memcpy(out16, c->counters.data(), 16 * sizeof(unsigned long long));
