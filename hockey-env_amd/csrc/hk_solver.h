@@ -428,9 +428,11 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
   for (int k = 0; k < 9; ++k) sb[k] = 0u;
   bool active = nc > 0;
   int it = 0;
-  for (; it < kVelIters && active; ++it) {
-    S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
-    if ((it & 3) == 3) {
+  static_assert(kVelIters % 4 == 0, "the snapshot period divides the iteration count");
+  for (; it < kVelIters && active; it += 4) {  // 4 iterations per trip: the snapshot period
+#pragma unroll
+    for (int u = 0; u < 4; ++u) S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
+    {
       uint32_t diff = 0u;
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
@@ -449,7 +451,7 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
         s.sn[2] = x2;
         s.sn[3] = x3;
       });
-      if (it >= 7 && diff == 0u) active = false;
+      if (it + 3 >= 7 && diff == 0u) active = false;
     }
   }
   return it;
