@@ -281,9 +281,13 @@ HK_DEV bool pair_far_collide(const Arena &w, int p) {
   const float dx = cA.x - cB.x, dy = cA.y - cB.y;
   return dx * dx + dy * dy > lim * lim;
 }
+// b2TimeOfImpact can only report TOUCHING when the GJK core distance falls below target + tolerance
+// (< rA + rB) at some t.  B's core stays within rcore of its COM, which moves on the segment c0 -> c, so the
+// box gap between that swept disc's AABB and A's core AABB bounds the core distance from below: a gap above
+// rA + rB (+ margin) means alpha = 1 exactly, without running the iteration.
 HK_DEV bool pair_far_toi(const Arena &w, int p) {  // static A, dynamic B, sweeps already aligned
   const int fA = SC.pairA[p], fB = SC.pairB[p], bB = SC.pbodyB[p];
-  const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
+  const float reach = SC.fx[fA].radius + SC.fx[fB].radius + kFarMargin;
   const float r = SC.rcore[bB];
   const float c0x = pick(w.d.c0x, bB, 0.0f), c0y = pick(w.d.c0y, bB, 0.0f);
   const float cx = pick(w.d.cx, bB, 0.0f), cy = pick(w.d.cy, bB, 0.0f);
