@@ -19,7 +19,7 @@ def per_launch(counter):
     for fn in files:
         with open(fn) as f:
             for row in csv.DictReader(f):
-                if "step_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                if "step_kernel<false>" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     if not vals:
         sys.exit(f"no {counter} rows for step_kernel in {files}")

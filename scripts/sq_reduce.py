@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 acc = collections.defaultdict(list)
 for fn in glob.glob(os.path.join(ROOT, "gpurun_out", "sq_*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(fn)):
-        if "step_kernel" in row["Kernel_Name"]:
+        if "step_kernel<false>" in row["Kernel_Name"]:
             acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
 avg = {k: sum(v) / len(v) for k, v in acc.items()}
 for k in sorted(avg):
