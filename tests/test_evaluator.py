@@ -1,0 +1,65 @@
+"""§8 row f4: checkpoint interop (reference TD3 checkpoint layout, weights-only loading) and the reference's
+evaluation protocol (rl/utils/evaluator.py:10-35) run on GPU arenas, pinned against the reference
+notebook's recorded 1000-game BasicOpponent study (Hockey-Env.ipynb:999, :2088-2154: 150.9 steps/game,
+winners +1/0/-1 = 319/368/313).  The reference's own trained checkpoints are not copied into this repo;
+`load_actor` reads any such file at run time."""
+import numpy as np
+import pytest
+import torch
+
+from hockey_amd.evaluate import Actor, load_actor, reset_params
+
+
+def _fake_checkpoint(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    actor = Actor()
+    with torch.no_grad():
+        for p in actor.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.2)
+    critic = {"action_low": -torch.ones(4), "action_high": torch.ones(4), "q1.fc1.weight": torch.zeros(256, 22)}
+    return {"policy": actor.state_dict(), "critic": critic, "target_policy": actor.state_dict(),
+            "target_critic": critic}, actor
+
+
+def test_load_actor_reference_layout(tmp_path):
+    ck, ref = _fake_checkpoint()
+    path = tmp_path / "td3_best.pt"
+    torch.save(ck, path)
+    actor = load_actor(str(path), device="cpu")
+    x = torch.randn(64, 18)
+    assert torch.equal(actor(x), ref(x))
+    with pytest.raises(ValueError):
+        load_actor({"critic": ck["critic"]}, device="cpu")
+
+
+def test_reset_protocol_alternates_side():
+    p, max_t, one = reset_params(6, 42)
+    assert max_t == 250 and list(one) == [False, True, False, True, False, True]
+    # puck on player 2's half when one_starts is False (hockey_env.py:381-392)
+    assert all((p[i, 2] > 5.0) == (not one[i]) for i in range(6))
+
+
+@pytest.mark.gpu
+def test_basic_vs_basic_matches_notebook_study():
+    from hockey_amd.evaluate import evaluate
+
+    n = 2000
+    r = evaluate(None, episodes=n, seed=0, player1="strong")
+    sd = lambda p: np.sqrt(p * (1 - p) / n)  # noqa: E731
+    assert abs(r["win"] - 0.319) < 4 * sd(0.319) + 0.02, r
+    assert abs(r["loss"] - 0.313) < 4 * sd(0.313) + 0.02, r
+    assert abs(r["draw"] - 0.368) < 4 * sd(0.368) + 0.02, r
+    assert abs(r["mean_length"] - 150.9) < 8.0, r
+
+
+@pytest.mark.gpu
+def test_checkpoint_policy_evaluation_runs(tmp_path):
+    from hockey_amd.evaluate import evaluate
+
+    ck, _ = _fake_checkpoint(1)
+    path = tmp_path / "td3_last.pt"
+    torch.save(ck, path)
+    actor = load_actor(str(path), device="cuda:0")
+    r = evaluate(actor, episodes=256, seed=42, weak_opponent=True)
+    assert abs(r["win"] + r["draw"] + r["loss"] - 1.0) < 1e-9
+    assert 1.0 <= r["mean_length"] <= 251.0 and np.isfinite(r["mean_return"])
