@@ -28,9 +28,9 @@ namespace hk {
 #define SC g_scene
 
 // register-resident solver slots.  Strong-vs-strong statistics (host build, 2.4M arena-steps): island
-// solves with 0/1/2/3/4+ contacts 70.3/29.7/1.5/0.02/<0.001 %, TOI mini-islands with 1/2 contacts
+// solves with 0/1/2/3/4+ contacts 70.3/29.7/1.5/0.02/3e-4 %, TOI mini-islands with 1/2 contacts
 // 99.7/0.3 %.  Larger solves take the HBM slot file (HbmSlots), bit-identically.
-constexpr int kIslandC = 3;
+constexpr int kIslandC = 4;
 constexpr int kToiC = 2;
 constexpr int kBigC = kMaxIsland;  // generic solver bound (geometric max is 9)
 constexpr uint32_t kEdgeMask[3] = {(1u << 8) | (1u << 10) | (0xFFu << 11),   // player1: 8, 10, 11..18
