@@ -120,7 +120,12 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
   get_vel(B, bA, vA, wA);
   get_vel(B, bB, vB, wB);
   xform xA, xB;
-  xA.q = rot_set(aA);
+  if (bA >= 3) {  // static body: angle +0, rot_set(+0) == (+0, 1)
+    xA.q.s = 0.0f;
+    xA.q.c = 1.0f;
+  } else {
+    xA.q = rot_set(aA);
+  }
   xB.q = rot_set(aB);
   xA.p = vsub(cA, mul_rv(xA.q, local_center(bA)));
   xB.p = vsub(cB, mul_rv(xB.q, local_center(bB)));
@@ -317,7 +322,13 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
   for (int j = 0; j < 2; ++j) {
     if (j < pcount) {
       xform xA, xB;
-      xA.q = rot_set(aA);
+      // a static body stays at angle +0 (iA == 0 keeps aA bit-exact), and rot_set(+0) == (+0, 1)
+      if (bA >= 3) {
+        xA.q.s = 0.0f;
+        xA.q.c = 1.0f;
+      } else {
+        xA.q = rot_set(aA);
+      }
       xB.q = rot_set(aB);
       xA.p = vsub(cA, mul_rv(xA.q, lcA));
       xB.p = vsub(cB, mul_rv(xB.q, lcB));
