@@ -602,7 +602,7 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
 HK_DEV float toi_pair(Arena &w, int p) {
   const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
   const float alpha0 = pick(w.d.al0, bB, 0.0f);  // == max(alpha0 A, alpha0 B) after alignment
-  const Proxy<kStaticVerts> pA = make_proxy<kStaticVerts>(SC.fx[SC.pairA[p]]);
+  const Proxy<kStaticVerts, true> pA = make_proxy<kStaticVerts, true>(SC.fx[SC.pairA[p]]);
   const Proxy<kMaxPolyVerts> pB = make_proxy<kMaxPolyVerts>(SC.fx[SC.pairB[p]]);
   float beta;
   const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);

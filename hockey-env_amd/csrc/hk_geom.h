@@ -247,15 +247,16 @@ HK_DEV void collide_polygons(Manifold &m, const RFix<NA> &pA, xform xfA, const R
 // Register proxies: the fixture's vertices are copied into registers once per query (statics have <= 4
 // vertices, players 7, the puck 1), so GJK / TOI iterations run on registers instead of re-loading
 // vertices from memory with per-lane addresses.  Vertex fetch by index is a select chain.
-template <int N>
+template <int N, bool kStaticBody = false>
 struct Proxy {
+  static constexpr bool kStatic = kStaticBody;  // the fixture's body never moves (sweep c0 == c, angle 0)
   float vx[N], vy[N];
   int count;
   float radius;
 };
-template <int N>
-HK_DEV Proxy<N> make_proxy(const Fixture &f) {
-  Proxy<N> p;
+template <int N, bool kStaticBody = false>
+HK_DEV Proxy<N, kStaticBody> make_proxy(const Fixture &f) {
+  Proxy<N, kStaticBody> p;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     p.vx[k] = f.vx[k];
@@ -265,8 +266,8 @@ HK_DEV Proxy<N> make_proxy(const Fixture &f) {
   p.radius = f.radius;
   return p;
 }
-template <int N>
-HK_DEV v2 pv(const Proxy<N> &p, int i) {
+template <int N, bool S>
+HK_DEV v2 pv(const Proxy<N, S> &p, int i) {
   float x = p.vx[0], y = p.vy[0];
 #pragma unroll
   for (int k = 1; k < N; ++k) {
@@ -277,8 +278,8 @@ HK_DEV v2 pv(const Proxy<N> &p, int i) {
   return V(x, y);
 }
 // b2DistanceProxy::GetSupport: first vertex with the strictly largest projection
-template <int N>
-HK_DEV int proxy_support(const Proxy<N> &p, v2 d) {
+template <int N, bool S>
+HK_DEV int proxy_support(const Proxy<N, S> &p, v2 d) {
   int best = 0;
   float bv = dot(V(p.vx[0], p.vy[0]), d);
 #pragma unroll
@@ -465,6 +466,19 @@ HK_DEV void sweep_xf(const Sweep &s, xform &xf, float beta) {
   xf.q = rot_set(angle);
   xf.p = vsub(xf.p, mul_rv(xf.q, s.lc));
 }
+// b2Sweep::GetTransform of the proxy's body: a static body has a0 == a == +0 and local centre 0, so the
+// angle interpolates to +0 exactly, rot_set(+0) == (+0, 1) and the centre offset subtracts +0 -- only the
+// position interpolation remains (it is kept: (1-b)*c0 + b*c need not round to c).
+template <typename P>
+HK_DEV void sweep_xf_of(const Sweep &s, xform &xf, float beta) {
+  if constexpr (P::kStatic) {
+    xf.p = vadd(vs(1.0f - beta, s.c0), vs(beta, s.c));
+    xf.q.s = 0.0f;
+    xf.q.c = 1.0f;
+  } else {
+    sweep_xf(s, xf, beta);
+  }
+}
 HK_DEV void sweep_advance(Sweep &s, float alpha) {
   float beta = (alpha - s.alpha0) / (1.0f - s.alpha0);
   s.c0 = vadd(s.c0, vs(beta, vsub(s.c, s.c0)));
@@ -493,8 +507,8 @@ HK_DEV void sep_init(SepFn<PA, PB> &f, const SimplexCache &cache, const PA &pA, 
                      const Sweep &sB, float t1) {
   f.pA = pA; f.pB = pB; f.sA = sA; f.sB = sB;
   xform xA, xB;
-  sweep_xf(f.sA, xA, t1);
-  sweep_xf(f.sB, xB, t1);
+  sweep_xf_of<PA>(f.sA, xA, t1);
+  sweep_xf_of<PB>(f.sB, xB, t1);
   if (cache.count == 1) {
     f.type = SF_POINTS;
     v2 a = mul_xv(xA, pv(pA, cache.iA[0]));
@@ -528,8 +542,8 @@ HK_DEV void sep_init(SepFn<PA, PB> &f, const SimplexCache &cache, const PA &pA, 
 template <typename PA, typename PB>
 HK_DEV float sep_find_min(const SepFn<PA, PB> &f, int &iA, int &iB, float t) {
   xform xA, xB;
-  sweep_xf(f.sA, xA, t);
-  sweep_xf(f.sB, xB, t);
+  sweep_xf_of<PA>(f.sA, xA, t);
+  sweep_xf_of<PB>(f.sB, xB, t);
   if (f.type == SF_POINTS) {
     v2 axA = mulT_rv(xA.q, f.axis), axB = mulT_rv(xB.q, vneg(f.axis));
     iA = proxy_support(f.pA, axA);
@@ -557,8 +571,8 @@ HK_DEV float sep_find_min(const SepFn<PA, PB> &f, int &iA, int &iB, float t) {
 template <typename PA, typename PB>
 HK_DEV float sep_eval(const SepFn<PA, PB> &f, int iA, int iB, float t) {
   xform xA, xB;
-  sweep_xf(f.sA, xA, t);
-  sweep_xf(f.sB, xB, t);
+  sweep_xf_of<PA>(f.sA, xA, t);
+  sweep_xf_of<PB>(f.sB, xB, t);
   if (f.type == SF_POINTS) {
     v2 a = mul_xv(xA, pv(f.pA, iA)), b = mul_xv(xB, pv(f.pB, iB));
     return dot(vsub(b, a), f.axis);
@@ -593,8 +607,8 @@ HK_DEV int time_of_impact(const PA &pA, const PB &pB, Sweep sA, Sweep sB, float 
   cache.metric = 0.0f;
   for (;;) {
     xform xA, xB;
-    sweep_xf(sA, xA, t1);
-    sweep_xf(sB, xB, t1);
+    sweep_xf_of<PA>(sA, xA, t1);
+    sweep_xf_of<PB>(sB, xB, t1);
     float dist = gjk_distance(cache, pA, xA, pB, xB, 0);
     if (dist <= 0.0f) { state = TOI_OVERLAPPED; t_out = 0.0f; break; }
     if (dist < target + tol) { state = TOI_TOUCHING; t_out = t1; break; }
