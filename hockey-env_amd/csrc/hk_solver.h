@@ -219,13 +219,10 @@ HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
 }
 
 // one b2ContactSolver::SolveVelocityConstraints pass over one contact
-HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
+// the body-velocity-local form: vA, wA, vB, wB are the two bodies' velocities, updated in place
+HK_DEV void fslot_solve_velocity_v(FSlot &s, v2 &vA, float &wA, v2 &vB, float &wB) {
   const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
-  const int bA = fs_bA(s), bB = fs_bB(s), vcount = fs_vcount(s);
-  v2 vA, vB;
-  float wA, wB;
-  get_vel(B, bA, vA, wA);
-  get_vel(B, bB, vB, wB);
+  const int vcount = fs_vcount(s);
   const v2 normal = V(s.nx, s.ny), tangent = crs_vs(normal, 1.0f);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -302,6 +299,15 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
       s.ni[1] = x.y;
     }
   }
+}
+
+HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
+  const int bA = fs_bA(s), bB = fs_bB(s);
+  v2 vA, vB;
+  float wA, wB;
+  get_vel(B, bA, vA, wA);
+  get_vel(B, bB, vB, wB);
+  fslot_solve_velocity_v(s, vA, wA, vB, wB);
   set_vel(B, bA, vA, wA);
   set_vel(B, bB, vB, wB);
 }
@@ -384,6 +390,8 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
 //             budget nor use private (scratch) memory.
 template <int C>
 struct RegSlots {
+  static constexpr bool kRegister = true;
+  static constexpr bool kOneFast = (C == kToiC);  // the TOI mini-island solve (islands: register budget)
   FSlot s[C];
   ManGeo g[C];  // position-phase geometry, loaded once per position loop (load_geo)
   HK_DEV void load_geo(int nc, const Arena &w) {
@@ -405,6 +413,8 @@ struct RegSlots {
 };
 
 struct HbmSlots {
+  static constexpr bool kRegister = false;
+  static constexpr bool kOneFast = false;
   float *ws;
   int64_t n, a;
   HK_DEV float &word(int i, int k) const { return ws[((int64_t)i * kSlotWords + k) * n + a]; }
@@ -431,9 +441,54 @@ template <typename SL> struct SlotCap;
 template <int C> struct SlotCap<RegSlots<C>> { static constexpr int value = C; };
 template <> struct SlotCap<HbmSlots> { static constexpr int value = kBigC; };
 
+// One-contact solve (the common case, and the usual owner of a wave's 180-iteration tail): the two bodies'
+// velocities stay in locals for the whole loop instead of round-tripping through the body file's selects
+// every iteration.  A static body's velocity is re-read as +0 at every iteration, exactly what get_vel
+// returns in the general loop; the snapshot compares the same values the general loop compares.
+HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
+  const int bA = fs_bA(s), bB = fs_bB(s);
+  const bool dynA = bA < 3;
+  v2 vA, vB;
+  float wA, wB;
+  get_vel(B, bA, vA, wA);
+  get_vel(B, bB, vB, wB);
+  uint32_t sn[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) sn[k] = 0u;
+  int it = 0;
+  bool active = true;
+  for (; it < kVelIters && active; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!dynA) {
+        vA = V(0.0f, 0.0f);
+        wA = 0.0f;
+      }
+      fslot_solve_velocity_v(s, vA, wA, vB, wB);
+    }
+    const uint32_t x[10] = {__float_as_uint(vB.x), __float_as_uint(vB.y), __float_as_uint(wB),
+                            dynA ? __float_as_uint(vA.x) : 0u, dynA ? __float_as_uint(vA.y) : 0u,
+                            dynA ? __float_as_uint(wA) : 0u, __float_as_uint(s.ni[0]), __float_as_uint(s.ni[1]),
+                            __float_as_uint(s.ti[0]), __float_as_uint(s.ti[1])};
+    uint32_t diff = 0u;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      diff |= x[k] ^ sn[k];
+      sn[k] = x[k];
+    }
+    if (it + 3 >= 7 && diff == 0u) active = false;
+  }
+  if (dynA) set_vel(B, bA, vA, wA);
+  set_vel(B, bB, vB, wB);
+  return it;
+}
+
 // 180 velocity iterations over nc slots, with the exact periodic early exit
 template <typename SL>
 HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
+  if constexpr (SL::kRegister && SL::kOneFast) {
+    if (nc == 1) return velocity_iterations_one(S.s[0], B);
+  }
   uint32_t sb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) sb[k] = 0u;
