@@ -270,12 +270,49 @@ HK_DEV void apply_torque(Arena &w, float t) {
 HK_DEV float box_gap(float ax0, float ay0, float ax1, float ay1, const float *b) {
   return fmaxf(fmaxf(b[0] - ax1, ax0 - b[2]), fmaxf(b[1] - ay1, ay0 - b[3]));
 }
-HK_DEV bool pair_far_collide(const Arena &w, int p) {
+// Axis-aligned box around a player's core (radius-free polygon) relative to its COM at the rotation q:
+// {min x, min y, max x, max y} of R(q) (v_i - lc).  Second stage of the far tests below: the bounding disc
+// (rcore) is loose for the elongated racket, and a player parked in front of its own goal otherwise sends
+// its goal and goal-side wall pairs to the narrow phase / b2TimeOfImpact every step, where they come out
+// separated (oracle statistics: ~90 % of b2TimeOfImpact calls).
+HK_DEV void player_core_box(const Arena &w, int f, int b, float q_s, float q_c, float (&e)[4]) {
+  e[0] = e[1] = kFltMax;
+  e[2] = e[3] = -kFltMax;
+#pragma unroll
+  for (int k = 0; k < kMaxPolyVerts; ++k) {
+    if (k < SC.fx[f].count) {
+      const float ux = SC.fx[f].vx[k] - SC.lcx[b], uy = SC.fx[f].vy[k] - SC.lcy[b];
+      const float rx = q_c * ux - q_s * uy, ry = q_s * ux + q_c * uy;
+      e[0] = fminf(e[0], rx); e[1] = fminf(e[1], ry);
+      e[2] = fmaxf(e[2], rx); e[3] = fmaxf(e[3], ry);
+    }
+  }
+}
+// both players' core boxes at their current rotations, computed once per pass over the pair table
+struct CoreBoxes {
+  float e[2][4];
+};
+HK_DEV void core_boxes(const Arena &w, CoreBoxes &cb) {
+  player_core_box(w, F_P1, B_P1, w.d.qs[B_P1], w.d.qc[B_P1], cb.e[0]);
+  player_core_box(w, F_P2, B_P2, w.d.qs[B_P2], w.d.qc[B_P2], cb.e[1]);
+}
+HK_DEV bool static_far_collide(int fA, int bB, v2 cB, const float (&e)[4], float reach) {
+  return box_gap(cB.x + e[0], cB.y + e[1], cB.x + e[2], cB.y + e[3], SC.fx_aabb[fA]) > reach;
+}
+// cb: the players' core boxes when the caller has them (pair-table passes), else computed here
+HK_DEV bool pair_far_collide(const Arena &w, int p, const CoreBoxes *cb = nullptr) {
   const int fA = SC.pairA[p], fB = SC.pairB[p], bA = SC.pbodyA[p], bB = SC.pbodyB[p];
   const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
   const v2 cB = body_c(w, bB);
   const float rB = SC.rcore[bB];
-  if (bA >= 3) return box_gap(cB.x - rB, cB.y - rB, cB.x + rB, cB.y + rB, SC.fx_aabb[fA]) > reach;
+  if (bA >= 3) {
+    if (box_gap(cB.x - rB, cB.y - rB, cB.x + rB, cB.y + rB, SC.fx_aabb[fA]) > reach) return true;
+    if (bB == B_PK) return false;  // a circle's core is its centre: the disc test is already exact
+    if (cb) return static_far_collide(fA, bB, cB, cb->e[bB == B_P2 ? 1 : 0], reach);
+    float e[4];
+    player_core_box(w, fB, bB, pick(w.d.qs, bB, 0.0f), pick(w.d.qc, bB, 1.0f), e);
+    return static_far_collide(fA, bB, cB, e, reach);
+  }
   const v2 cA = body_c(w, bA);
   const float lim = SC.rcore[bA] + rB + reach;
   const float dx = cA.x - cB.x, dy = cA.y - cB.y;
@@ -285,14 +322,21 @@ HK_DEV bool pair_far_collide(const Arena &w, int p) {
 // (< rA + rB) at some t.  B's core stays within rcore of its COM, which moves on the segment c0 -> c, so the
 // box gap between that swept disc's AABB and A's core AABB bounds the core distance from below: a gap above
 // rA + rB (+ margin) means alpha = 1 exactly, without running the iteration.
-HK_DEV bool pair_far_toi(const Arena &w, int p) {  // static A, dynamic B, sweeps already aligned
+// For a player the second stage bounds its core by the exact box at the end-of-sweep rotation q = rot(a)
+// (the transform is synchronised with the sweep whenever the scan runs), widened by rcore * |a - a0|:
+// a core point moves at most that far as the angle runs over [a0, a].
+HK_DEV bool pair_far_toi(const Arena &w, int p, const CoreBoxes &cb) {  // static A, dynamic B, sweeps aligned
   const int fA = SC.pairA[p], fB = SC.pairB[p], bB = SC.pbodyB[p];
   const float reach = SC.fx[fA].radius + SC.fx[fB].radius + kFarMargin;
   const float r = SC.rcore[bB];
   const float c0x = pick(w.d.c0x, bB, 0.0f), c0y = pick(w.d.c0y, bB, 0.0f);
   const float cx = pick(w.d.cx, bB, 0.0f), cy = pick(w.d.cy, bB, 0.0f);
-  return box_gap(fminf(c0x, cx) - r, fminf(c0y, cy) - r, fmaxf(c0x, cx) + r, fmaxf(c0y, cy) + r,
-                 SC.fx_aabb[fA]) > reach;
+  const float lx = fminf(c0x, cx), ly = fminf(c0y, cy), hx = fmaxf(c0x, cx), hy = fmaxf(c0y, cy);
+  if (box_gap(lx - r, ly - r, hx + r, hy + r, SC.fx_aabb[fA]) > reach) return true;
+  if (bB == B_PK) return false;  // circle: exact already
+  const float(&e)[4] = cb.e[bB == B_P2 ? 1 : 0];
+  const float rot = r * fabsf(pick(w.d.a, bB, 0.0f) - pick(w.d.a0, bB, 0.0f));
+  return box_gap(lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot, SC.fx_aabb[fA]) > reach;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -407,14 +451,19 @@ HK_DEV void pair_update(Arena &w, int p) {
 HK_DEV void collide(Arena &w) {
   if (w.d.awake[0] && w.d.awake[1] && w.d.awake[2]) {
     uint32_t near = 0u;
+    CoreBoxes cb;
+    core_boxes(w, cb);
     for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
-      if (pair_far_collide(w, p)) pair_update_far(w, p);
+      if (pair_far_collide(w, p, &cb)) pair_update_far(w, p);
       else near |= 1u << p;
     }
     while (near) {
       const int p = __ffs(near) - 1;
       near &= near - 1u;
       pair_update_near(w, p);
+#ifdef HK_X_DUP_NEAR
+      { int p2 = p; asm volatile("" : "+v"(p2)); pair_update_near(w, p2); }
+#endif
     }
     return;
   }
@@ -611,11 +660,18 @@ HK_DEV float toi_pair(Arena &w, int p) {
 #endif
   return st == TOI_TOUCHING ? fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f) : 1.0f;
 }
-HK_DEV void toi_drain(Arena &w, uint32_t &pending) {
+// runs the lane's queued b2TimeOfImpact calls in pair order; `below` tracks the pairs whose cached alpha is
+// below 1 (the only ones the minimum selection can pick: it starts at 1 and compares strictly)
+HK_DEV void toi_drain(Arena &w, uint32_t &pending, uint32_t &below) {
   while (pending) {
     const int p = __ffs(pending) - 1;
     pending &= pending - 1u;
-    LDS(w, kLdsToi + p) = toi_pair(w, p);
+    float alpha = toi_pair(w, p);
+#ifdef HK_X_DUP_TOI
+    { int p2 = p; asm volatile("" : "+v"(p2)); const float a2 = toi_pair(w, p2); asm volatile("" :: "v"(a2)); }
+#endif
+    LDS(w, kLdsToi + p) = alpha;
+    below = alpha < 1.0f ? (below | (1u << p)) : (below & ~(1u << p));
   }
 }
 
@@ -623,13 +679,11 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
 #pragma unroll
   for (int b = 0; b < 3; ++b) w.d.al0[b] = 0.0f;
   for (int k = 0; k < 8; ++k) LDS(w, kLdsSal0 + k) = 0.0f;
-  for (int p = 0; p < NP; ++p) {
-    LDS(w, kLdsToi + p) = 1.0f;
-    LDS(w, kLdsCnt + p) = 0.0f;
-  }
+  for (int p = 0; p < NP; ++p) LDS(w, kLdsCnt + p) = 0.0f;  // TOI alphas: only read below 1 (`below`)
   w.toiflag = 0u;
   w.cisl = 0u;
   w.bisl = 0u;
+  uint32_t below = 0u;  // pairs whose cached TOI alpha (LDS) is < 1
   for (;;) {
     HK_TIC(T, 5);  // diagnostics: events / min selection -> "toi-events"
     // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
@@ -639,6 +693,8 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     //     TOIs therefore see exactly the sweeps the sequential scan would.  Should a dynamic body ever be
     //     advanced here, its lane first drains its queue so the sequential order is kept regardless.
     uint32_t elig = 0u, pending = 0u;
+    CoreBoxes cb;  // the players' poses are fixed during the pass (only sweep starts move)
+    core_boxes(w, cb);
     for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
       const uint32_t bit = 1u << p;
       if (!(w.enabled & bit)) continue;
@@ -657,13 +713,13 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
       if (a0A < a0B) {
         LDS(w, kLdsSal0 + bA - 3) = a0B;  // static b2Sweep::Advance: only alpha0 moves
       } else if (a0B < a0A) {
-        toi_drain(w, pending);  // keep the sequential order for this lane (see above)
+        toi_drain(w, pending, below);  // keep the sequential order for this lane (see above)
         Sweep sw = body_sweep(w, bB);
         sweep_advance(sw, a0A);
         body_set_sweep(w, bB, sw);
       }
-      if (pair_far_toi(w, p)) {
-        LDS(w, kLdsToi + p) = 1.0f;
+      if (pair_far_toi(w, p, cb)) {
+        below &= ~bit;  // alpha 1
       } else {
         pending |= bit;
       }
@@ -671,13 +727,14 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     HK_TIC(T, 6);  // diagnostics: scan pass -> "toi-scan"
     // (2) per-lane queue: every lane runs b2TimeOfImpact on its own next pair (lanes stay converged on
     //     the same code instead of serialising over the union of the wave's pairs)
-    toi_drain(w, pending);
+    toi_drain(w, pending, below);
     HK_TIC(T, 7);  // diagnostics: b2TimeOfImpact -> "toi-solve" slot
-    // (3) Box2D's minimum: first pair (in order) with the smallest alpha
+    // (3) Box2D's minimum: first pair (in order) with the smallest alpha.  Pairs at alpha 1 never win the
+    //     strict comparison, so only the lane's eligible pairs below 1 are visited (usually none or one).
     int minc = -1;
     float minAlpha = 1.0f;
-    for (int p = 0; p < NP; ++p) {
-      if (!((elig >> p) & 1u)) continue;
+    for (uint32_t m = elig & below; m; m &= m - 1u) {
+      const int p = __ffs(m) - 1;
       const float alpha = LDS(w, kLdsToi + p);
       if (alpha < minAlpha) { minc = p; minAlpha = alpha; }
     }
