@@ -13,7 +13,7 @@
 //   * the 3 dynamic bodies live in register arrays (Dyn), indexed with compile-time indices or through
 //     3-way selects for a runtime body id; static bodies are compile-time scene data (__constant__);
 //   * contact state is bitmasks over the 27-pair table (touching / enabled / TOI / island flags);
-//   * Box2D manifolds stay in HBM (DevState::man, [slot][field][arena], lane-contiguous) and are read
+//   * Box2D manifolds stay in HBM (DevState::man, 64-B records [slot][arena], see man_rec) and are read
 //     or written in place where Box2D reads or writes them;
 //   * per-pair TOI alphas / sub-step counts and the static bodies' sweep alpha0 live in LDS
 //     ([k][64 lanes], conflict-free for any k);
@@ -123,7 +123,14 @@ HK_DEV void place(T (&x)[3], int b, T v) {
   x[2] = (b == 2) ? v : x2;
 }
 HK_DEV float &LDS(Arena &w, int k) { return w.lds[k * 64 + w.lane]; }
-HK_DEV float &MF(const Arena &w, int slot, int field) { return w.man[((int64_t)slot * NMF + field) * w.n + w.a]; }
+// Box2D manifold record of solid-pair slot `slot` for this arena: [slot][arena][16 words].  A lane's
+// record is one 64-B block, so the per-lane (divergent) slot accesses of the near-pair / island / TOI
+// queues touch one cache line per record instead of one per field; lanes on the same slot read 4 KiB
+// contiguous per wave.  Accesses are whole 16-B quads (global_load/store_dwordx4).
+struct alignas(16) Quad { float x, y, z, w; };
+HK_DEV Quad *man_rec(const Arena &w, int slot) {
+  return reinterpret_cast<Quad *>(w.man + ((int64_t)slot * w.n + w.a) * NMF);
+}
 
 HK_DEV float inv_mass(int b) { return b < 3 ? SC.invMass[b] : 0.0f; }
 HK_DEV float inv_inertia(int b) { return b < 3 ? SC.invI[b] : 0.0f; }
@@ -382,19 +389,20 @@ HK_DEV void pair_update_near(Arena &w, int p) {
       }
       touching = m.count > 0;
       if (touching) {
-        const int slot = SC.manslot[p];
+        Quad *rec = man_rec(w, SC.manslot[p]);
         // match old contact ids to carry impulses (the stored manifold is meaningful only if touching)
         int oc = 0;
         uint32_t oid0 = 0u, oid1 = 0u;
         float oni0 = 0.0f, oni1 = 0.0f, oti0 = 0.0f, oti1 = 0.0f;
         if (was) {
-          oc = __float_as_int(MF(w, slot, M_META)) & 0xff;
-          oid0 = (uint32_t)__float_as_int(MF(w, slot, M_P0ID));
-          oni0 = MF(w, slot, M_P0NI);
-          oti0 = MF(w, slot, M_P0TI);
-          oid1 = (uint32_t)__float_as_int(MF(w, slot, M_P1ID));
-          oni1 = MF(w, slot, M_P1NI);
-          oti1 = MF(w, slot, M_P1TI);
+          const Quad q0 = rec[0], q2 = rec[2], q3 = rec[3];
+          oc = __float_as_int(q0.x) & 0xff;
+          oid0 = (uint32_t)__float_as_int(q2.y);
+          oid1 = (uint32_t)__float_as_int(q2.z);
+          oni0 = q3.x;
+          oti0 = q3.y;
+          oni1 = q3.z;
+          oti1 = q3.w;
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -405,22 +413,14 @@ HK_DEV void pair_update_near(Arena &w, int p) {
             else if (oc > 1 && oid1 == m.id[i]) { m.ni[i] = oni1; m.ti[i] = oti1; }
           }
         }
-        MF(w, slot, M_META) = __int_as_float(m.count | (m.type << 8));
-        MF(w, slot, M_LNX) = m.ln.x;
-        MF(w, slot, M_LNY) = m.ln.y;
-        MF(w, slot, M_LPX) = m.lp.x;
-        MF(w, slot, M_LPY) = m.lp.y;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (j < m.count) {
-            const int o = M_P0X + j * 5;
-            MF(w, slot, o + 0) = m.pt_lp[j].x;
-            MF(w, slot, o + 1) = m.pt_lp[j].y;
-            MF(w, slot, o + 2) = __int_as_float((int)m.id[j]);
-            MF(w, slot, o + 3) = m.ni[j];
-            MF(w, slot, o + 4) = m.ti[j];
-          }
-        }
+        // whole-record write; a one-point manifold's point-1 words are zeroed (every reader is bounded by
+        // the point count, as in Box2D)
+        const bool two = m.count > 1;
+        rec[0] = Quad{__int_as_float(m.count | (m.type << 8)), m.ln.x, m.ln.y, m.lp.x};
+        rec[1] = Quad{m.lp.y, m.pt_lp[0].x, m.pt_lp[0].y, two ? m.pt_lp[1].x : 0.0f};
+        rec[2] = Quad{two ? m.pt_lp[1].y : 0.0f, __int_as_float((int)m.id[0]), two ? __int_as_float((int)m.id[1]) : 0,
+                      0.0f};
+        rec[3] = Quad{m.ni[0], m.ti[0], two ? m.ni[1] : 0.0f, two ? m.ti[1] : 0.0f};
       }
       if (touching != was) { set_awake(w, bA, 1); set_awake(w, bB, 1); }
     }

@@ -36,10 +36,8 @@ struct Ctx {
   int device = 0;
   hk::DevState s{};
   hk::KCfg cfg{};
-  bool scene_ok = false;
 };
 
-bool g_scene_uploaded[64] = {false};
 
 int check_policy(int p) { return p >= HK_POLICY_EXTERNAL && p <= HK_POLICY_BASIC_STRONG; }
 
@@ -100,15 +98,6 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
       (e = hipMalloc(&c->s.ws, nw * 4)) != hipSuccess || (e = hipMalloc(&c->s.counters, HK_NUM_COUNTERS * 8)) != hipSuccess) {
     hk_destroy(c);
     return hipfail(e, "hk_create: hipMalloc");
-  }
-  if (device < 64 && !g_scene_uploaded[device]) {
-    hk::Scene sc;
-    hk::build_scene(sc);
-    if ((e = hk::upload_scene(sc)) != hipSuccess) {
-      hk_destroy(c);
-      return hipfail(e, "hk_create: scene upload");
-    }
-    g_scene_uploaded[device] = true;
   }
   if ((e = hipMemset(c->s.counters, 0, HK_NUM_COUNTERS * 8)) != hipSuccess ||
       (e = hipMemset(c->s.man, 0, nm * 4)) != hipSuccess) {

@@ -7,8 +7,8 @@
 //   hockey/hockey_env.py:781-833  BasicOpponent.act (fused policy)
 // Float operation order follows Box2D 2.3 / the reference's numpy+pybox2d semantics exactly; the file is
 // compiled with -ffp-contract=off and IEEE div/sqrt so results are bit-identical to the CPU oracle
-// (tests/test_gpu_parity.py).  Scene constants (hulls, normals, masses) are computed once on the host
-// (hk_scene.cpp) and live in __constant__ memory.
+// (tests/test_gpu_parity.py).  Scene constants (hulls, normals, masses) are computed on the host at build
+// time (hk_scene.cpp via hk_scene_gen.cpp) and compiled in as a constexpr Scene.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -213,6 +213,13 @@ HK_DEV double hk_cos(double x) {
     default: return ksin(a, b);
   }
 }
+
+// Analysis build only (-DHK_ASM_MARKS): labels in the device assembly around hot regions.
+#ifdef HK_ASM_MARKS
+#define HK_MARK(x) asm volatile(";HKMARK " #x)
+#else
+#define HK_MARK(x) ((void)0)
+#endif
 
 // Diagnostic build only (make TIMERS=1): per-phase shader-clock accounting; compiled out otherwise.
 #ifdef HK_PHASE_TIMERS

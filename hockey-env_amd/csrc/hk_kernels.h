@@ -12,14 +12,17 @@ enum { FB_PX = 0, FB_PY, FB_CX, FB_CY, FB_A, FB_VX, FB_VY, FB_W, FB_SLEEP, FB };
 enum { F_PFX = 3 * FB, F_PFY, NFF };
 // int fields
 enum { I_AWAKE = 0, I_HAS1, I_HAS2, I_TIME, I_DONE, I_WINNER, I_MAXT, I_TOUCH, I_ENABLED, I_ONE, I_EPISODE, I_STEP, NIF };
-// manifold fields per solid pair
-enum { M_META = 0, M_LNX, M_LNY, M_LPX, M_LPY, M_P0X, M_P0Y, M_P0ID, M_P0NI, M_P0TI, M_P1X, M_P1Y, M_P1ID, M_P1NI,
-       M_P1TI, NMF };
+// manifold record per (solid pair, arena): 16 words = 64 B, read / written as four 16-B quads
+//   q0 {meta, local normal x, y, local point x}   q1 {local point y, point0 x, y, point1 x}
+//   q2 {point1 y, id0, id1, pad}                  q3 {normal impulse 0, tangent impulse 0, normal 1, tangent 1}
+enum { M_META = 0, M_LNX, M_LNY, M_LPX, M_LPY, M_P0X, M_P0Y, M_P1X, M_P1Y, M_P0ID, M_P1ID, M_PAD, M_P0NI, M_P0TI,
+       M_P1NI, M_P1TI, NMF };
+static_assert(NMF == 16, "a manifold record is four 16-byte quads");
 
 struct DevState {
   float *f;
   int32_t *i;
-  float *man;
+  float *man;  // manifold records [NSOLID][N][NMF] (64 B per record, hk_arena.h ManRec)
   float *ws;  // large-island slot workspace [kBigC][kSlotWords][N] (hk_solver.h HbmSlots)
   double *phase;
   unsigned long long *counters;
@@ -51,11 +54,11 @@ hipError_t launch_observe(const DevState &s, const KCfg &cfg, float *obs, float 
 hipError_t launch_get_state(const DevState &s, const KCfg &cfg, float *state, int32_t *aux, hipStream_t st);
 hipError_t launch_set_state(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *state,
                             const int32_t *aux, hipStream_t st);
-hipError_t upload_scene(const Scene &sc);
 int64_t workspace_words_per_arena();
 
 // host-side scene construction (hk_scene.cpp): Box2D 2.3 hull / normals / mass data of hockey_env.py's
-// fixtures, and the canonical contact pair table.
+// fixtures, and the canonical contact pair table.  Run at build time by hk_scene_gen.cpp, whose output
+// (hk_scene_data.inc) is the kernels' compile-time scene.
 void build_scene(Scene &sc);
 
 }  // namespace hk

@@ -71,23 +71,24 @@ struct ManGeo {
   v2 ln, lp, pt[2];
 };
 HK_DEV ManGeo man_geo(const Arena &w, int p) {
-  const int slot = SC.manslot[p];
+  const Quad *rec = man_rec(w, SC.manslot[p]);
+  const Quad q0 = rec[0], q1 = rec[1], q2 = rec[2];
   ManGeo g;
-  const int meta = __float_as_int(MF(w, slot, M_META));
+  const int meta = __float_as_int(q0.x);
   g.count = meta & 0xff;
   g.type = meta >> 8;
-  g.ln = V(MF(w, slot, M_LNX), MF(w, slot, M_LNY));
-  g.lp = V(MF(w, slot, M_LPX), MF(w, slot, M_LPY));
-  g.pt[0] = V(MF(w, slot, M_P0X), MF(w, slot, M_P0Y));
-  g.pt[1] = g.count > 1 ? V(MF(w, slot, M_P1X), MF(w, slot, M_P1Y)) : V(0.0f, 0.0f);
+  g.ln = V(q0.y, q0.z);
+  g.lp = V(q0.w, q1.x);
+  g.pt[0] = V(q1.y, q1.z);
+  g.pt[1] = g.count > 1 ? V(q1.w, q2.x) : V(0.0f, 0.0f);
   return g;
 }
 
 // b2ContactSolver constructor for one contact
 HK_DEV void fslot_load(FSlot &s, const Arena &w, int p, int warm, int isl) {
   const int pa = SC.pbodyA[p], pb = SC.pbodyB[p];
-  const int slot = SC.manslot[p];
-  const int meta = __float_as_int(MF(w, slot, M_META));
+  const Quad *rec = man_rec(w, SC.manslot[p]);
+  const int meta = __float_as_int(rec[0].x);
   const int count = meta & 0xff, type = meta >> 8;
   s.bits = p | (isl << 5) | (pa << 7) | (pb << 11) | (count << 15) | (count << 17) | (type << 19);
   s.fr = SC.friction[p];
@@ -95,12 +96,14 @@ HK_DEV void fslot_load(FSlot &s, const Arena &w, int p, int warm, int isl) {
   s.Kxx = s.Kxy = s.Kyy = 0.0f;
   s.Nxx = s.Nxy = s.Nyy = 0.0f;
   s.nx = s.ny = 0.0f;
+  Quad q3 = Quad{0.0f, 0.0f, 0.0f, 0.0f};
+  if (warm) q3 = rec[3];
+  const float mni[2] = {q3.x, q3.z}, mti[2] = {q3.y, q3.w};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const bool on = j < count;
-    const int o = M_P0X + j * 5;
-    s.ni[j] = on && warm ? 1.0f * MF(w, slot, o + 3) : 0.0f;
-    s.ti[j] = on && warm ? 1.0f * MF(w, slot, o + 4) : 0.0f;
+    s.ni[j] = on && warm ? 1.0f * mni[j] : 0.0f;
+    s.ti[j] = on && warm ? 1.0f * mti[j] : 0.0f;
     s.rAx[j] = s.rAy[j] = s.rBx[j] = s.rBy[j] = 0.0f;
     s.nm[j] = s.tm[j] = s.bias[j] = 0.0f;
   }
@@ -457,6 +460,7 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
   for (int k = 0; k < 10; ++k) sn[k] = 0u;
   int it = 0;
   bool active = true;
+  HK_MARK(vone_begin);
   for (; it < kVelIters && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -478,6 +482,7 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
     }
     if (it + 3 >= 7 && diff == 0u) active = false;
   }
+  HK_MARK(vone_end);
   if (dynA) set_vel(B, bA, vA, wA);
   set_vel(B, bB, vB, wB);
   return it;
@@ -495,6 +500,7 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
   bool active = nc > 0;
   int it = 0;
   static_assert(kVelIters % 4 == 0, "the snapshot period divides the iteration count");
+  HK_MARK(vit_begin);
   for (; it < kVelIters && active; it += 4) {  // 4 iterations per trip: the snapshot period
 #pragma unroll
     for (int u = 0; u < 4; ++u) S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
@@ -520,18 +526,19 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
       if (it + 3 >= 7 && diff == 0u) active = false;
     }
   }
+  HK_MARK(vit_end);
   return it;
 }
 
-HK_DEV void fslot_store(const FSlot &s, Arena &w) {
-  const int slot = SC.manslot[fs_pair(s)];
+HK_DEV void fslot_store(const FSlot &s, Arena &w) {  // b2ContactSolver::StoreImpulses (j < pointCount)
+  float *q3 = reinterpret_cast<float *>(man_rec(w, SC.manslot[fs_pair(s)]) + 3);
   const int vcount = fs_vcount(s);
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-    if (j < vcount) {
-      MF(w, slot, M_P0X + j * 5 + 3) = s.ni[j];
-      MF(w, slot, M_P0X + j * 5 + 4) = s.ti[j];
-    }
+  if (vcount == 2) {
+    *reinterpret_cast<Quad *>(q3) = Quad{s.ni[0], s.ti[0], s.ni[1], s.ti[1]};
+  } else if (vcount == 1) {
+    q3[0] = s.ni[0];
+    q3[1] = s.ti[0];
+  }
 }
 
 HK_DEV void integrate_one(float h, Dyn &B, int b) {

@@ -7,7 +7,8 @@
 //                               sleep time} + the puck's pending force (TRAIN_DEFENSE reset)
 //   i[NIF][N]            int32  awake bits, has_puck1/2, time, done, winner, max_t, touching mask,
 //                               enabled mask, one_starts, episode and step counters
-//   man[NSOLID][NMF][N]  float  Box2D manifold of every solid pair (read/written in place, touching only)
+//   man[NSOLID][N][NMF]  float  Box2D manifold record (64 B) of every solid pair (read/written in place,
+//                               touching only; hk_arena.h man_rec)
 //   phase[2][N]          double BasicOpponent phases (global np.random stream -> per-arena Philox)
 #pragma once
 #include "hk_arena.h"
@@ -43,9 +44,6 @@ enum { RNG_ACTION = 1, RNG_PHASE = 2, RNG_RESET = 3, RNG_PHASE0 = 4 };
 // ------------------------------------------------------------------------------------------------
 HK_DEV float &F(const DevState &s, int field, int64_t a) { return s.f[(int64_t)field * s.n + a]; }
 HK_DEV int32_t &I(const DevState &s, int field, int64_t a) { return s.i[(int64_t)field * s.n + a]; }
-HK_DEV float &M(const DevState &s, int slot, int field, int64_t a) {
-  return s.man[((int64_t)slot * NMF + field) * s.n + a];
-}
 
 HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, int vel_ref, float *lds, int lane) {
   const int awake = I(s, I_AWAKE, a);

@@ -31,10 +31,11 @@ static inline double __hiloint2double(int hi, int lo) {
 
 #include "../hk_core.h"
 
-hk::Scene g_scene;  // host copy of the __constant__ scene
+constexpr hk::Scene g_scene =  // the kernels' compile-time scene (hk_scene_gen.cpp)
+#include "../hk_scene_data.inc"
+    ;
 
 #include "../hk_step.h"
-#include "../hk_scene.cpp"
 
 using namespace hk;
 
@@ -53,8 +54,6 @@ extern "C" {
 
 // cfg = {keep_mode, mode, auto_reset, vel_ref, policy0, policy1}; seed; arena_offset
 void *hkh_create(int64_t n, const int *cfg6, uint64_t seed, int64_t arena_offset) {
-  static bool scene_ready = false;
-  if (!scene_ready) { build_scene(g_scene); scene_ready = true; }
   HostCtx *c = new HostCtx();
   c->n = n;
   c->f.assign((size_t)NFF * n, 0.0f);
