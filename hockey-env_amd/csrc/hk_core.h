@@ -101,6 +101,18 @@ HK_DEV float vnormalize(v2 &a) {
   a.y *= inv;
   return l;
 }
+// Packed 2-vectors (v_pk_mul_f32 / v_pk_add_f32): per component the same IEEE fp32 operation as the
+// scalar form, so results are bit-identical; one wave issues a packed op at ~1.2x the cost of a scalar
+// one (scripts/micro/pk_issue.hip), i.e. ~1.7x the fp32 throughput.  Used in the hot contact-solver loops.
+typedef float f2 __attribute__((vector_size(8)));  // GCC/clang vector extension (the host harness is g++)
+HK_DEV f2 F2(v2 a) { return f2{a.x, a.y}; }
+HK_DEV v2 V2(f2 a) { return V(a[0], a[1]); }
+HK_DEV f2 bc(float s) { return f2{s, s}; }
+// crs_sv(s, r) == bc(s) * perp(r) bit for bit: (-s) * y == s * (-y) (negation commutes with rounding)
+HK_DEV f2 perp(f2 r) { return f2{-r[1], r[0]}; }
+HK_DEV float pdot(f2 a, f2 b) { const f2 p = a * b; return p[0] + p[1]; }                // dot()
+HK_DEV float pcrs(f2 a, f2 b) { const f2 p = a * f2{b[1], b[0]}; return p[0] - p[1]; }  // crs()
+
 HK_DEV float fmin2(float a, float b) { return a < b ? a : b; }
 HK_DEV float fmax2(float a, float b) { return a > b ? a : b; }
 HK_DEV float fclamp(float a, float lo, float hi) { return fmax2(lo, fmin2(a, hi)); }

@@ -304,15 +304,99 @@ HK_DEV void fslot_solve_velocity_v(FSlot &s, v2 &vA, float &wA, v2 &vB, float &w
   }
 }
 
+// fslot_solve_velocity_v on packed body velocities: the same float operations in the same order, with the
+// 2-vector arithmetic issued as packed fp32 instructions
+HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &wB) {
+  const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
+  const int vcount = fs_vcount(s);
+  const f2 normal = f2{s.nx, s.ny}, tangent = f2{1.0f * s.ny, -1.0f * s.nx};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j < vcount) {
+      const f2 rA = f2{s.rAx[j], s.rAy[j]}, rB = f2{s.rBx[j], s.rBy[j]};
+      const f2 dv = ((vB + bc(wB) * perp(rB)) - vA) - bc(wA) * perp(rA);
+      float vt = pdot(dv, tangent) - 0.0f;
+      float lambda = s.tm[j] * (-vt);
+      float maxF = s.fr * s.ni[j];
+      float newI = fclamp(s.ti[j] + lambda, -maxF, maxF);
+      lambda = newI - s.ti[j];
+      s.ti[j] = newI;
+      const f2 P = bc(lambda) * tangent;
+      vA = vA - bc(mA) * P;
+      wA -= iA * pcrs(rA, P);
+      vB = vB + bc(mB) * P;
+      wB += iB * pcrs(rB, P);
+    }
+  }
+  if (vcount == 1) {
+    const f2 rA = f2{s.rAx[0], s.rAy[0]}, rB = f2{s.rBx[0], s.rBy[0]};
+    const f2 dv = ((vB + bc(wB) * perp(rB)) - vA) - bc(wA) * perp(rA);
+    float vn = pdot(dv, normal);
+    float lambda = -s.nm[0] * (vn - s.bias[0]);
+    float newI = fmax2(s.ni[0] + lambda, 0.0f);
+    lambda = newI - s.ni[0];
+    s.ni[0] = newI;
+    const f2 P = bc(lambda) * normal;
+    vA = vA - bc(mA) * P;
+    wA -= iA * pcrs(rA, P);
+    vB = vB + bc(mB) * P;
+    wB += iB * pcrs(rB, P);
+  } else {
+    const f2 r1A = f2{s.rAx[0], s.rAy[0]}, r1B = f2{s.rBx[0], s.rBy[0]};
+    const f2 r2A = f2{s.rAx[1], s.rAy[1]}, r2B = f2{s.rBx[1], s.rBy[1]};
+    v2 a = V(s.ni[0], s.ni[1]);
+    const f2 dv1 = ((vB + bc(wB) * perp(r1B)) - vA) - bc(wA) * perp(r1A);
+    const f2 dv2 = ((vB + bc(wB) * perp(r2B)) - vA) - bc(wA) * perp(r2A);
+    float vn1 = pdot(dv1, normal), vn2 = pdot(dv2, normal);
+    v2 b;
+    b.x = vn1 - s.bias[0];
+    b.y = vn2 - s.bias[1];
+    b = vsub(b, V(s.Kxx * a.x + s.Kxy * a.y, s.Kxy * a.x + s.Kyy * a.y));
+    v2 x = vneg(V(s.Nxx * b.x + s.Nxy * b.y, s.Nxy * b.x + s.Nyy * b.y));
+    int ok = 0;
+    if (x.x >= 0.0f && x.y >= 0.0f) ok = 1;
+    if (!ok) {
+      x.x = -s.nm[0] * b.x;
+      x.y = 0.0f;
+      vn2 = s.Kxy * x.x + b.y;
+      if (x.x >= 0.0f && vn2 >= 0.0f) ok = 1;
+    }
+    if (!ok) {
+      x.x = 0.0f;
+      x.y = -s.nm[1] * b.y;
+      vn1 = s.Kxy * x.y + b.x;
+      if (x.y >= 0.0f && vn1 >= 0.0f) ok = 1;
+    }
+    if (!ok) {
+      x.x = 0.0f;
+      x.y = 0.0f;
+      vn1 = b.x;
+      vn2 = b.y;
+      if (vn1 >= 0.0f && vn2 >= 0.0f) ok = 1;
+    }
+    if (ok) {
+      const v2 d = vsub(x, a);
+      const f2 P1 = bc(d.x) * normal, P2 = bc(d.y) * normal;
+      vA = vA - bc(mA) * (P1 + P2);
+      wA -= iA * (pcrs(r1A, P1) + pcrs(r2A, P2));
+      vB = vB + bc(mB) * (P1 + P2);
+      wB += iB * (pcrs(r1B, P1) + pcrs(r2B, P2));
+      s.ni[0] = x.x;
+      s.ni[1] = x.y;
+    }
+  }
+}
+
 HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s);
   v2 vA, vB;
   float wA, wB;
   get_vel(B, bA, vA, wA);
   get_vel(B, bB, vB, wB);
-  fslot_solve_velocity_v(s, vA, wA, vB, wB);
-  set_vel(B, bA, vA, wA);
-  set_vel(B, bB, vB, wB);
+  f2 pA = F2(vA), pB = F2(vB);
+  fslot_solve_velocity_p(s, pA, wA, pB, wB);
+  set_vel(B, bA, V2(pA), wA);
+  set_vel(B, bB, V2(pB), wB);
 }
 
 // one NGS position pass over one contact (b2ContactSolver::SolvePositionConstraints body).  In this scene
@@ -451,10 +535,11 @@ template <> struct SlotCap<HbmSlots> { static constexpr int value = kBigC; };
 HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s);
   const bool dynA = bA < 3;
-  v2 vA, vB;
+  v2 vA2, vB2;
   float wA, wB;
-  get_vel(B, bA, vA, wA);
-  get_vel(B, bB, vB, wB);
+  get_vel(B, bA, vA2, wA);
+  get_vel(B, bB, vB2, wB);
+  f2 vA = F2(vA2), vB = F2(vB2);
   uint32_t sn[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) sn[k] = 0u;
@@ -465,13 +550,13 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!dynA) {
-        vA = V(0.0f, 0.0f);
+        vA = f2{0.0f, 0.0f};
         wA = 0.0f;
       }
-      fslot_solve_velocity_v(s, vA, wA, vB, wB);
+      fslot_solve_velocity_p(s, vA, wA, vB, wB);
     }
-    const uint32_t x[10] = {__float_as_uint(vB.x), __float_as_uint(vB.y), __float_as_uint(wB),
-                            dynA ? __float_as_uint(vA.x) : 0u, dynA ? __float_as_uint(vA.y) : 0u,
+    const uint32_t x[10] = {__float_as_uint(vB[0]), __float_as_uint(vB[1]), __float_as_uint(wB),
+                            dynA ? __float_as_uint(vA[0]) : 0u, dynA ? __float_as_uint(vA[1]) : 0u,
                             dynA ? __float_as_uint(wA) : 0u, __float_as_uint(s.ni[0]), __float_as_uint(s.ni[1]),
                             __float_as_uint(s.ti[0]), __float_as_uint(s.ti[1])};
     uint32_t diff = 0u;
@@ -483,8 +568,8 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
     if (it + 3 >= 7 && diff == 0u) active = false;
   }
   HK_MARK(vone_end);
-  if (dynA) set_vel(B, bA, vA, wA);
-  set_vel(B, bB, vB, wB);
+  if (dynA) set_vel(B, bA, V2(vA), wA);
+  set_vel(B, bB, V2(vB), wB);
   return it;
 }
 
