@@ -371,6 +371,16 @@ HK_DEV void pair_update_near(Arena &w, int p) {
   const uint32_t bit = 1u << p;
   const int was = (w.touch & bit) != 0u;
   w.enabled |= bit;
+  // the stored manifold (ids / impulses) of a touching pair is requested before the narrow phase so its
+  // HBM / L2 latency overlaps the clipping arithmetic
+  const int slot = SC.manslot[p];
+  Quad o0 = Quad{0.0f, 0.0f, 0.0f, 0.0f}, o2 = o0, o3 = o0;
+  if (slot >= 0 && was) {
+    const Quad *orec = man_rec(w, slot);
+    o0 = orec[0];
+    o2 = orec[2];
+    o3 = orec[3];
+  }
   int touching;
   {
     const xform xA = body_xf(w, bA), xB = body_xf(w, bB);
@@ -389,20 +399,19 @@ HK_DEV void pair_update_near(Arena &w, int p) {
       }
       touching = m.count > 0;
       if (touching) {
-        Quad *rec = man_rec(w, SC.manslot[p]);
+        Quad *rec = man_rec(w, slot);
         // match old contact ids to carry impulses (the stored manifold is meaningful only if touching)
         int oc = 0;
         uint32_t oid0 = 0u, oid1 = 0u;
         float oni0 = 0.0f, oni1 = 0.0f, oti0 = 0.0f, oti1 = 0.0f;
         if (was) {
-          const Quad q0 = rec[0], q2 = rec[2], q3 = rec[3];
-          oc = __float_as_int(q0.x) & 0xff;
-          oid0 = (uint32_t)__float_as_int(q2.y);
-          oid1 = (uint32_t)__float_as_int(q2.z);
-          oni0 = q3.x;
-          oti0 = q3.y;
-          oni1 = q3.z;
-          oti1 = q3.w;
+          oc = __float_as_int(o0.x) & 0xff;
+          oid0 = (uint32_t)__float_as_int(o2.y);
+          oid1 = (uint32_t)__float_as_int(o2.z);
+          oni0 = o3.x;
+          oti0 = o3.y;
+          oni1 = o3.z;
+          oti1 = o3.w;
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {

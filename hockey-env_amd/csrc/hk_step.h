@@ -352,7 +352,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   out.nbig = w.n_big;
 #ifdef HK_PHASE_TIMERS
   if (io.debug) {  // diagnostics build: per-lane work counters
-    float *d = io.debug + a * 8;
+    float *d = io.debug + a * 16;
     d[1] = (float)w.n_toi; d[2] = (float)w.dg_vit_isl; d[3] = (float)w.dg_vit_toi; d[4] = (float)w.dg_pit;
     d[5] = (float)w.dg_toi_calls; d[6] = (float)w.dg_nc_max; d[7] = (float)w.n_big;
   }
