@@ -38,6 +38,9 @@ def _args():
     ap.add_argument("--rollout", type=int, default=50,
                     help="also time hk_rollout with this many steps per launch (0 = skip); reported under 'rollout'")
     ap.add_argument("--cpu-arenas", type=int, default=32768, help="CPU baseline sample: arenas x 250 steps")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
+                         "reported under 'streams'")
     return ap.parse_args()
 
 
@@ -116,6 +119,56 @@ def _time_rollout(env, N, torch, dist, world, dev, args):
             "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3}
 
 
+def _time_streams(args, N, torch, dist, world, rank, dev, pol):
+    """The same N arenas as S shard contexts (global arena ids unchanged, so every arena's trajectory is
+    the single-context one) stepped by hk_step on S HIP streams: each call still advances its shard by one
+    step, but one shard's slowest wave no longer idles the SIMDs the other shards' steps can use."""
+    from hockey_amd.vec_env import VecHockeyEnv
+
+    S, n = args.streams, args.arenas
+    if n % S:
+        return None
+    m = n // S
+    envs, ios, streams = [], [], []
+    for k in range(S):
+        e = VecHockeyEnv(m, device=dev, policies=pol, auto_reset=True, seed=args.seed,
+                         arena_offset=shard_offset(rank, n) + k * m)
+        e.reset()
+        io = N.StepIO()
+        io.obs, io.reward, io.done, io.info = (e.obs_buf.data_ptr(), e.reward_buf.data_ptr(),
+                                               e.done_buf.data_ptr(), e.info_buf.data_ptr())
+        envs.append(e)
+        ios.append(io)
+        streams.append(torch.cuda.Stream(dev))
+    torch.cuda.synchronize()
+
+    def run(steps):
+        for _ in range(steps):
+            for e, io, st in zip(envs, ios, streams):
+                with torch.cuda.stream(st):
+                    e.step_raw(io)
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    for e in envs:
+        e.close()
+    return {"streams": S, "arenas_per_stream": m, "value": n * world * args.steps / elapsed,
+            "unit": "env-steps/s", "ms_per_step": elapsed / args.steps * 1e3}
+
+
 def main():
     args = _args()
     import torch
@@ -171,6 +224,9 @@ def main():
     rollout = None
     if args.rollout > 1:
         rollout = _time_rollout(env, N, torch, dist, world, dev, args)
+    streams = None
+    if args.streams > 1:
+        streams = _time_streams(args, N, torch, dist, world, rank, dev, pol)
     total_steps = n * world * args.steps
     assert int(cnt[N.CNT_STEPS]) == total_steps, (cnt, total_steps)
     assert int(cnt[N.CNT_OVERFLOW]) == 0, cnt
@@ -206,6 +262,8 @@ def main():
         }
         if rollout is not None:
             line["rollout"] = rollout
+        if streams is not None:
+            line["streams"] = streams
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas)
         print(json.dumps(line), flush=True)
