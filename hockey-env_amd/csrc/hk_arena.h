@@ -26,6 +26,13 @@
 namespace hk {
 
 #define SC g_scene
+// The scene again, as the step kernel's LDS copy (hk_kernels.hip: g_scene_lds, filled at kernel start).
+// Scene data indexed by a per-lane (divergent) pair / fixture / body id is read from here: a ds_read instead
+// of a gather through the vector L1 from the code object's constant table.  Compile-time and wave-uniform
+// indices keep using SC (instruction literals / scalar loads).
+#ifndef SLDS
+#define SLDS g_scene_lds
+#endif
 
 // register-resident solver slots.  Strong-vs-strong statistics (host build, 2.4M arena-steps): island
 // solves with 0/1/2/3/4+ contacts 70.3/29.7/1.5/0.02/3e-4 %, TOI mini-islands with 1/2 contacts
@@ -132,9 +139,10 @@ HK_DEV Quad *man_rec(const Arena &w, int slot) {
   return reinterpret_cast<Quad *>(w.man + ((int64_t)slot * w.n + w.a) * NMF);
 }
 
-HK_DEV float inv_mass(int b) { return b < 3 ? SC.invMass[b] : 0.0f; }
-HK_DEV float inv_inertia(int b) { return b < 3 ? SC.invI[b] : 0.0f; }
-HK_DEV v2 local_center(int b) { return b < 3 ? V(SC.lcx[b], SC.lcy[b]) : V(0.0f, 0.0f); }
+// per-lane body id -> dynamic-body constants by select (a static body reads 0)
+HK_DEV float inv_mass(int b) { return pick(SC.invMass, b, 0.0f); }
+HK_DEV float inv_inertia(int b) { return pick(SC.invI, b, 0.0f); }
+HK_DEV v2 local_center(int b) { return V(pick(SC.lcx, b, 0.0f), pick(SC.lcy, b, 0.0f)); }
 
 HK_DEV xform body_xf(const Arena &w, int b) {
   xform x;
@@ -143,14 +151,14 @@ HK_DEV xform body_xf(const Arena &w, int b) {
     x.q.s = pick(w.d.qs, b, 0.0f);
     x.q.c = pick(w.d.qc, b, 1.0f);
   } else {
-    x.p = V(SC.spx[b], SC.spy[b]);
+    x.p = V(SLDS.spx[b], SLDS.spy[b]);
     x.q.s = 0.0f;  // rot_set(0) == (+0, 1)
     x.q.c = 1.0f;
   }
   return x;
 }
 HK_DEV v2 body_c(const Arena &w, int b) {
-  return b < 3 ? V(pick(w.d.cx, b, 0.0f), pick(w.d.cy, b, 0.0f)) : V(SC.spx[b], SC.spy[b]);
+  return b < 3 ? V(pick(w.d.cx, b, 0.0f), pick(w.d.cy, b, 0.0f)) : V(SLDS.spx[b], SLDS.spy[b]);
 }
 HK_DEV Sweep body_sweep(Arena &w, int b) {
   Sweep s;
@@ -163,7 +171,7 @@ HK_DEV Sweep body_sweep(Arena &w, int b) {
     s.alpha0 = pick(w.d.al0, b, 0.0f);
   } else {  // static: c0 == c == origin and a0 == a == 0 forever; only alpha0 moves (b2Sweep::Advance)
     s.lc = V(0.0f, 0.0f);
-    s.c0 = s.c = V(SC.spx[b], SC.spy[b]);
+    s.c0 = s.c = V(SLDS.spx[b], SLDS.spy[b]);
     s.a0 = s.a = 0.0f;
     s.alpha0 = LDS(w, kLdsSal0 + b - 3);
   }
@@ -282,13 +290,14 @@ HK_DEV float box_gap(float ax0, float ay0, float ax1, float ay1, const float *b)
 // (rcore) is loose for the elongated racket, and a player parked in front of its own goal otherwise sends
 // its goal and goal-side wall pairs to the narrow phase / b2TimeOfImpact every step, where they come out
 // separated (oracle statistics: ~90 % of b2TimeOfImpact calls).
-HK_DEV void player_core_box(const Arena &w, int f, int b, float q_s, float q_c, float (&e)[4]) {
+HK_DEV void player_core_box(const Arena &w, int f, int b, float q_s, float q_c, float (&e)[4],
+                            const Scene &S = SC) {
   e[0] = e[1] = kFltMax;
   e[2] = e[3] = -kFltMax;
 #pragma unroll
   for (int k = 0; k < kMaxPolyVerts; ++k) {
-    if (k < SC.fx[f].count) {
-      const float ux = SC.fx[f].vx[k] - SC.lcx[b], uy = SC.fx[f].vy[k] - SC.lcy[b];
+    if (k < S.fx[f].count) {
+      const float ux = S.fx[f].vx[k] - S.lcx[b], uy = S.fx[f].vy[k] - S.lcy[b];
       const float rx = q_c * ux - q_s * uy, ry = q_s * ux + q_c * uy;
       e[0] = fminf(e[0], rx); e[1] = fminf(e[1], ry);
       e[2] = fmaxf(e[2], rx); e[3] = fmaxf(e[3], ry);
@@ -303,25 +312,26 @@ HK_DEV void core_boxes(const Arena &w, CoreBoxes &cb) {
   player_core_box(w, F_P1, B_P1, w.d.qs[B_P1], w.d.qc[B_P1], cb.e[0]);
   player_core_box(w, F_P2, B_P2, w.d.qs[B_P2], w.d.qc[B_P2], cb.e[1]);
 }
-HK_DEV bool static_far_collide(int fA, int bB, v2 cB, const float (&e)[4], float reach) {
-  return box_gap(cB.x + e[0], cB.y + e[1], cB.x + e[2], cB.y + e[3], SC.fx_aabb[fA]) > reach;
+HK_DEV bool static_far_collide(const Scene &S, int fA, int bB, v2 cB, const float (&e)[4], float reach) {
+  return box_gap(cB.x + e[0], cB.y + e[1], cB.x + e[2], cB.y + e[3], S.fx_aabb[fA]) > reach;
 }
 // cb: the players' core boxes when the caller has them (pair-table passes), else computed here
-HK_DEV bool pair_far_collide(const Arena &w, int p, const CoreBoxes *cb = nullptr) {
-  const int fA = SC.pairA[p], fB = SC.pairB[p], bA = SC.pbodyA[p], bB = SC.pbodyB[p];
-  const float reach = 2.0f * (SC.fx[fA].radius + SC.fx[fB].radius) + kFarMargin;
+// S: SC for a wave-uniform p (pair-table loops), SLDS for a per-lane p
+HK_DEV bool pair_far_collide(const Arena &w, int p, const CoreBoxes *cb = nullptr, const Scene &S = SC) {
+  const int fA = S.pairA[p], fB = S.pairB[p], bA = S.pbodyA[p], bB = S.pbodyB[p];
+  const float reach = 2.0f * (S.fx[fA].radius + S.fx[fB].radius) + kFarMargin;
   const v2 cB = body_c(w, bB);
-  const float rB = SC.rcore[bB];
+  const float rB = S.rcore[bB];
   if (bA >= 3) {
-    if (box_gap(cB.x - rB, cB.y - rB, cB.x + rB, cB.y + rB, SC.fx_aabb[fA]) > reach) return true;
+    if (box_gap(cB.x - rB, cB.y - rB, cB.x + rB, cB.y + rB, S.fx_aabb[fA]) > reach) return true;
     if (bB == B_PK) return false;  // a circle's core is its centre: the disc test is already exact
-    if (cb) return static_far_collide(fA, bB, cB, cb->e[bB == B_P2 ? 1 : 0], reach);
+    if (cb) return static_far_collide(S, fA, bB, cB, cb->e[bB == B_P2 ? 1 : 0], reach);
     float e[4];
-    player_core_box(w, fB, bB, pick(w.d.qs, bB, 0.0f), pick(w.d.qc, bB, 1.0f), e);
-    return static_far_collide(fA, bB, cB, e, reach);
+    player_core_box(w, fB, bB, pick(w.d.qs, bB, 0.0f), pick(w.d.qc, bB, 1.0f), e, S);
+    return static_far_collide(S, fA, bB, cB, e, reach);
   }
   const v2 cA = body_c(w, bA);
-  const float lim = SC.rcore[bA] + rB + reach;
+  const float lim = S.rcore[bA] + rB + reach;
   const float dx = cA.x - cB.x, dy = cA.y - cB.y;
   return dx * dx + dy * dy > lim * lim;
 }
@@ -349,8 +359,8 @@ HK_DEV bool pair_far_toi(const Arena &w, int p, const CoreBoxes &cb) {  // stati
 // ------------------------------------------------------------------------------------------------
 // ContactDetector.BeginContact (hockey_env.py:44-76) and b2Contact::Update
 // ------------------------------------------------------------------------------------------------
-HK_DEV void begin_contact(Arena &w, int p) {
-  const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+HK_DEV void begin_contact(Arena &w, int p) {  // per-lane p
+  const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
   const int hasPK = (bA == B_PK || bB == B_PK);
   if ((bA == B_G2 || bB == B_G2) && hasPK) { w.done = 1; w.winner = 1; }
   if ((bA == B_G1 || bB == B_G1) && hasPK) { w.done = 1; w.winner = -1; }
@@ -367,13 +377,13 @@ HK_DEV void begin_contact(Arena &w, int p) {
 // b2Contact::Update for a pair the broad phase could not reject: narrow phase, impulse carry-over,
 // wake-ups and BeginContact.
 HK_DEV void pair_update_near(Arena &w, int p) {
-  const int fA = SC.pairA[p], fB = SC.pairB[p], bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const int fA = SLDS.pairA[p], fB = SLDS.pairB[p], bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
   const uint32_t bit = 1u << p;
   const int was = (w.touch & bit) != 0u;
   w.enabled |= bit;
   // the stored manifold (ids / impulses) of a touching pair is requested before the narrow phase so its
   // HBM / L2 latency overlaps the clipping arithmetic
-  const int slot = SC.manslot[p];
+  const int slot = SLDS.manslot[p];
   Quad o0 = Quad{0.0f, 0.0f, 0.0f, 0.0f}, o2 = o0, o3 = o0;
   if (slot >= 0 && was) {
     const Quad *orec = man_rec(w, slot);
@@ -384,18 +394,18 @@ HK_DEV void pair_update_near(Arena &w, int p) {
   int touching;
   {
     const xform xA = body_xf(w, bA), xB = body_xf(w, bB);
-    if (SC.sensor[p]) {
-      touching = test_overlap(SC.fx[fA], xA, SC.fx[fB], xB);
+    if (SLDS.sensor[p]) {
+      touching = test_overlap(SLDS.fx[fA], xA, SLDS.fx[fB], xB);
     } else {
       Manifold m;
-      if (SC.fx[fB].circle) {  // puck: A is a static quad or a player
-        const RFix<1> cB = load_fix<1>(SC.fx[fB]);
-        if (bA >= 3) collide_poly_circle(m, load_fix<kStaticVerts>(SC.fx[fA]), xA, cB, xB);
-        else collide_poly_circle(m, load_fix<kMaxPolyVerts>(SC.fx[fA]), xA, cB, xB);
+      if (SLDS.fx[fB].circle) {  // puck: A is a static quad or a player
+        const RFix<1> cB = load_fix<1>(SLDS.fx[fB]);
+        if (bA >= 3) collide_poly_circle(m, load_fix<kStaticVerts>(SLDS.fx[fA]), xA, cB, xB);
+        else collide_poly_circle(m, load_fix<kMaxPolyVerts>(SLDS.fx[fA]), xA, cB, xB);
       } else {  // player B: A is a static quad or the other player
-        const RFix<kMaxPolyVerts> pB = load_fix<kMaxPolyVerts>(SC.fx[fB]);
-        if (bA >= 3) collide_polygons(m, load_fix<kStaticVerts>(SC.fx[fA]), xA, pB, xB);
-        else collide_polygons(m, load_fix<kMaxPolyVerts>(SC.fx[fA]), xA, pB, xB);
+        const RFix<kMaxPolyVerts> pB = load_fix<kMaxPolyVerts>(SLDS.fx[fB]);
+        if (bA >= 3) collide_polygons(m, load_fix<kStaticVerts>(SLDS.fx[fA]), xA, pB, xB);
+        else collide_polygons(m, load_fix<kMaxPolyVerts>(SLDS.fx[fA]), xA, pB, xB);
       }
       touching = m.count > 0;
       if (touching) {
@@ -439,16 +449,16 @@ HK_DEV void pair_update_near(Arena &w, int p) {
 }
 
 // b2Contact::Update for a pair the broad phase rejects: not touching (no manifold, no BeginContact)
-HK_DEV void pair_update_far(Arena &w, int p) {
+HK_DEV void pair_update_far(Arena &w, int p, const Scene &S = SC) {
   const uint32_t bit = 1u << p;
   const int was = (w.touch & bit) != 0u;
   w.enabled |= bit;
-  if (!SC.sensor[p] && was) { set_awake(w, SC.pbodyA[p], 1); set_awake(w, SC.pbodyB[p], 1); }
+  if (!S.sensor[p] && was) { set_awake(w, S.pbodyA[p], 1); set_awake(w, S.pbodyB[p], 1); }
   w.touch &= ~bit;
 }
 
-HK_DEV void pair_update(Arena &w, int p) {
-  if (pair_far_collide(w, p)) pair_update_far(w, p);
+HK_DEV void pair_update(Arena &w, int p) {  // per-lane p (TOI events)
+  if (pair_far_collide(w, p, nullptr, SLDS)) pair_update_far(w, p, SLDS);
   else pair_update_near(w, p);
 }
 
@@ -522,7 +532,7 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
         inis |= 1u << e;
         S.set_pair(nc, e, isl);
         ++nc;
-        const int pa = SC.pbodyA[e], pb = SC.pbodyB[e];
+        const int pa = SLDS.pbodyA[e], pb = SLDS.pbodyB[e];
         const int other = pa == bi ? pb : pa;
         if (other >= 3) continue;
         if (pick(island_of, other, 0) >= 0) continue;
@@ -658,10 +668,10 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
 
 // b2TimeOfImpact of static-vs-dynamic pair p (per-lane p) -> alpha in the step's [alpha0, 1] frame
 HK_DEV float toi_pair(Arena &w, int p) {
-  const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
+  const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
   const float alpha0 = pick(w.d.al0, bB, 0.0f);  // == max(alpha0 A, alpha0 B) after alignment
-  const Proxy<kStaticVerts, true> pA = make_proxy<kStaticVerts, true>(SC.fx[SC.pairA[p]]);
-  const Proxy<kMaxPolyVerts> pB = make_proxy<kMaxPolyVerts>(SC.fx[SC.pairB[p]]);
+  const Proxy<kStaticVerts, true> pA = make_proxy<kStaticVerts, true>(SLDS.fx[SLDS.pairA[p]]);
+  const Proxy<kMaxPolyVerts> pB = make_proxy<kMaxPolyVerts>(SLDS.fx[SLDS.pairB[p]]);
   float beta;
   const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);
 #ifdef HK_PHASE_TIMERS
@@ -749,7 +759,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     }
     if (minc < 0 || 1.0f - 10.0f * kFltEps < minAlpha) break;
     // ---- one TOI event (per-lane pair) ----
-    const int bA = SC.pbodyA[minc], bB = SC.pbodyB[minc];  // static A, dynamic B
+    const int bA = SLDS.pbodyA[minc], bB = SLDS.pbodyB[minc];  // static A, dynamic B
     const uint32_t mbit = 1u << minc;
     const Sweep backA = body_sweep(w, bA), backB = body_sweep(w, bB);
     body_advance(w, bA, minAlpha);
@@ -778,7 +788,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
       m &= m - 1u;
       const uint32_t ebit = 1u << e;
       if (w.cisl & ebit) continue;
-      const int other = SC.pbodyA[e] == bB ? SC.pbodyB[e] : SC.pbodyA[e];
+      const int other = SLDS.pbodyA[e] == bB ? SLDS.pbodyB[e] : SLDS.pbodyA[e];
       if (other < 3) continue;  // only static bodies join a TOI island
       const Sweep backup = body_sweep(w, other);
       if (!((w.bisl >> other) & 1u)) body_advance(w, other, minAlpha);

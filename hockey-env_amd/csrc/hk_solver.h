@@ -50,7 +50,7 @@ HK_DEV void get_pos(const Dyn &B, int b, v2 &c, float &a) {
     c = V(pick(B.cx, b, 0.0f), pick(B.cy, b, 0.0f));
     a = pick(B.a, b, 0.0f);
   } else {
-    c = V(SC.spx[b], SC.spy[b]);
+    c = V(SLDS.spx[b], SLDS.spy[b]);
     a = 0.0f;
   }
 }
@@ -71,7 +71,7 @@ struct ManGeo {
   v2 ln, lp, pt[2];
 };
 HK_DEV ManGeo man_geo(const Arena &w, int p) {
-  const Quad *rec = man_rec(w, SC.manslot[p]);
+  const Quad *rec = man_rec(w, SLDS.manslot[p]);
   const Quad q0 = rec[0], q1 = rec[1], q2 = rec[2];
   ManGeo g;
   const int meta = __float_as_int(q0.x);
@@ -86,12 +86,12 @@ HK_DEV ManGeo man_geo(const Arena &w, int p) {
 
 // b2ContactSolver constructor for one contact
 HK_DEV void fslot_load(FSlot &s, const Arena &w, int p, int warm, int isl) {
-  const int pa = SC.pbodyA[p], pb = SC.pbodyB[p];
-  const Quad *rec = man_rec(w, SC.manslot[p]);
+  const int pa = SLDS.pbodyA[p], pb = SLDS.pbodyB[p];
+  const Quad *rec = man_rec(w, SLDS.manslot[p]);
   const int meta = __float_as_int(rec[0].x);
   const int count = meta & 0xff, type = meta >> 8;
   s.bits = p | (isl << 5) | (pa << 7) | (pb << 11) | (count << 15) | (count << 17) | (type << 19);
-  s.fr = SC.friction[p];
+  s.fr = SLDS.friction[p];
   s.mA = inv_mass(pa); s.mB = inv_mass(pb); s.iA = inv_inertia(pa); s.iB = inv_inertia(pb);
   s.Kxx = s.Kxy = s.Kyy = 0.0f;
   s.Nxx = s.Nxy = s.Nyy = 0.0f;
@@ -159,7 +159,7 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
   }
   s.nx = normal.x;
   s.ny = normal.y;
-  const float re = SC.restitution[p];
+  const float re = SLDS.restitution[p];
   const int vcount = fs_vcount(s);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -616,7 +616,7 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
 }
 
 HK_DEV void fslot_store(const FSlot &s, Arena &w) {  // b2ContactSolver::StoreImpulses (j < pointCount)
-  float *q3 = reinterpret_cast<float *>(man_rec(w, SC.manslot[fs_pair(s)]) + 3);
+  float *q3 = reinterpret_cast<float *>(man_rec(w, SLDS.manslot[fs_pair(s)]) + 3);
   const int vcount = fs_vcount(s);
   if (vcount == 2) {
     *reinterpret_cast<Quad *>(q3) = Quad{s.ni[0], s.ti[0], s.ni[1], s.ti[1]};

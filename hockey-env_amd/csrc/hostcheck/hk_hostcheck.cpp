@@ -35,6 +35,7 @@ constexpr hk::Scene g_scene =  // the kernels' compile-time scene (hk_scene_gen.
 #include "../hk_scene_data.inc"
     ;
 
+#define SLDS g_scene  // the host build reads the one scene copy
 #include "../hk_step.h"
 
 using namespace hk;
