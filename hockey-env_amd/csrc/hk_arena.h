@@ -11,7 +11,8 @@
 //
 // State layout per lane:
 //   * the 3 dynamic bodies live in register arrays (Dyn), indexed with compile-time indices or through
-//     3-way selects for a runtime body id; static bodies are compile-time scene data (__constant__);
+//     3-way selects for a runtime body id; static bodies are compile-time scene data (constexpr Scene,
+//     and its LDS copy for per-lane ids);
 //   * contact state is bitmasks over the 27-pair table (touching / enabled / TOI / island flags);
 //   * Box2D manifolds stay in HBM (DevState::man, 64-B records [slot][arena], see man_rec) and are read
 //     or written in place where Box2D reads or writes them;

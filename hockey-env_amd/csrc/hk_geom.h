@@ -1,8 +1,8 @@
 // hk_geom.h -- Box2D 2.3 geometry for the hockey scene: narrow phase (b2CollidePolygonAndCircle,
 // b2CollidePolygons, b2ClipSegmentToLine), GJK distance (b2Distance / b2TestOverlap), sweeps and
 // conservative-advancement time of impact (b2TimeOfImpact, b2SeparationFunction).
-// All functions are register-resident: fixtures come from __constant__ memory, simplex vertices are
-// named (no runtime-indexed private arrays), so nothing here touches scratch memory.
+// All functions are register-resident: fixtures come from the compile-time scene (or its LDS copy),
+// simplex vertices are named (no runtime-indexed private arrays), so nothing here touches scratch memory.
 // Float operation order matches the CPU test oracle bit for bit.
 #pragma once
 #include "hk_core.h"
