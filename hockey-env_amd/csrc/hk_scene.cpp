@@ -1,4 +1,4 @@
-// hk_scene.cpp -- host construction of the static scene uploaded to __constant__ memory.
+// hk_scene.cpp -- host construction of the static scene (run at build time by hk_scene_gen.cpp).
 //
 // Geometry of hockey/hockey_env.py:183-343 (players :183-202, puck :204-220, walls/posts :222-319,
 // goals :321-343) turned into Box2D 2.3 shapes exactly as box2d-py would: vertices are computed in
