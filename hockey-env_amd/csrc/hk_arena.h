@@ -635,7 +635,7 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
 // contact edges in order).  Mass gating of SolveTOIPositionConstraints is therefore the identity.
 // ------------------------------------------------------------------------------------------------
 template <typename SL>
-HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, int db, float sub_dt) {
+HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, int db, float sub_dt, PhaseT &T) {
   uint32_t m = extra;
   S.each(nc, [&](FSlot &s, int i) {
     int p = minc;
@@ -651,12 +651,14 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
     });
     if (minSep >= -1.5f * kLinearSlop) break;
   }
+  HK_TIC(T, 10);  // diagnostics: TOI position passes
   // leap of faith (the static body's c0 already equals its c)
   place(w.d.c0x, db, pick(w.d.cx, db, 0.0f));
   place(w.d.c0y, db, pick(w.d.cy, db, 0.0f));
   place(w.d.a0, db, pick(w.d.a, db, 0.0f));
   S.each(nc, [&](FSlot &s, int) { fslot_init_velocity(s, w); });
   const int vit = velocity_iterations(S, w.d, nc);
+  HK_TIC(T, 11);  // diagnostics: TOI velocity iterations
 #ifdef HK_PHASE_TIMERS
   w.dg_vit_toi += vit;
 #endif
@@ -766,6 +768,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     body_advance(w, bA, minAlpha);
     body_advance(w, bB, minAlpha);
     pair_update(w, minc);
+    HK_TIC(T, 8);  // diagnostics: TOI event advance + contact update
     w.toiflag &= ~mbit;
     LDS(w, kLdsCnt + minc) += 1.0f;
     if (!(w.enabled & mbit) || !(w.touch & mbit)) {
@@ -803,15 +806,16 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
       ++nc;
       w.bisl |= 1u << other;
     }
+    HK_TIC(T, 9);  // diagnostics: TOI island build
     const float sub_dt = (1.0f - minAlpha) * dt;
     if (nc > kBigC) { w.overflow = 1; nc = kBigC; }
     if (nc <= kToiC && !w.force_big) {
       RegSlots<kToiC> S;
-      toi_island_solve(w, S, minc, extra, nc, bB, sub_dt);
+      toi_island_solve(w, S, minc, extra, nc, bB, sub_dt, T);
     } else {
       w.n_big++;
       HbmSlots S{w.ws, w.n, w.a};
-      toi_island_solve(w, S, minc, extra, nc, bB, sub_dt);
+      toi_island_solve(w, S, minc, extra, nc, bB, sub_dt, T);
     }
     // reset island flags; invalidate the TOIs of the displaced dynamic body
     w.bisl = 0u;

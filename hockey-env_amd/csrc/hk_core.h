@@ -236,7 +236,7 @@ HK_DEV double hk_cos(double x) {
 // Diagnostic build only (make TIMERS=1): per-phase shader-clock accounting; compiled out otherwise.
 #ifdef HK_PHASE_TIMERS
 struct PhaseT {
-  unsigned long long last, acc[8];
+  unsigned long long last, acc[13];
 };
 #define HK_TIC(T, k)                                              \
   do {                                                            \

@@ -343,7 +343,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   w.time += 1;
   store_arena(w, s, a);
   I(s, I_STEP, a) = (int)(stepc + 1);
-  HK_TIC(T, 5);
+  HK_TIC(T, 12);  // diagnostics: outputs and state store
   out.done_edge = (!was_done && w.done);
   out.win1 = out.done_edge && w.winner == 1;
   out.win2 = out.done_edge && w.winner == -1;
@@ -352,7 +352,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   out.nbig = w.n_big;
 #ifdef HK_PHASE_TIMERS
   if (io.debug) {  // diagnostics build: per-lane work counters
-    float *d = io.debug + a * 16;
+    float *d = io.debug + a * 24;
     d[1] = (float)w.n_toi; d[2] = (float)w.dg_vit_isl; d[3] = (float)w.dg_vit_toi; d[4] = (float)w.dg_pit;
     d[5] = (float)w.dg_toi_calls; d[6] = (float)w.dg_nc_max; d[7] = (float)w.n_big;
   }

@@ -17,7 +17,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 env = VecHockeyEnv(n, device="cuda:0", policies=("strong", "strong"), auto_reset=True, seed=1)
 env.reset()
-dbg = torch.zeros((n, 16), dtype=torch.float32, device="cuda:0")
+dbg = torch.zeros((n, 24), dtype=torch.float32, device="cuda:0")
 io = N.StepIO()
 io.obs = env.obs_buf.data_ptr()
 io.reward = env.reward_buf.data_ptr()
@@ -32,17 +32,17 @@ for s in range(steps):
     torch.cuda.synchronize()
     d = dbg.cpu().numpy().copy()
     rows.append(d)
-D = np.stack(rows)  # [steps, n, 16]: 0 wave cycles, 1-7 lane work, 8-15 wave phase cycles
+D = np.stack(rows)  # [steps, n, 24]: 0 wave cycles, 1-7 lane work, 8-19 wave phase cycles
 wave = D[:, ::64, 0]  # [steps, waves]
 print(f"wave cycles per step: mean {wave.mean():.0f}  median {np.median(wave):.0f}  p99 {np.percentile(wave, 99):.0f}  "
       f"max-per-step mean {wave.max(1).mean():.0f}")
-lanes = D.reshape(steps, n // 64, 64, 16)
+lanes = D.reshape(steps, n // 64, 64, 24)
 for q in (50, 90, 99):
     print(f"per-lane p{q}:", {nm: float(np.percentile(D[:, :, k], q)) for k, nm in enumerate(names) if k})
 print("per-lane max:", {nm: float(D[:, :, k].max()) for k, nm in enumerate(names) if k})
-PH = ["load+policy+presolve", "collide", "isl-setup", "isl-velocity", "isl-position+sleep", "toi-events+out",
-      "toi-scan", "toi-b2TOI"]
-ph = D[:, ::64, 8:16]  # [steps, waves, 8]
+PH = ["load+policy+presolve", "collide", "isl-setup", "isl-velocity", "isl-position+sleep", "toi-min",
+      "toi-scan", "toi-b2TOI", "toi-event-update", "toi-island-build", "toi-position", "toi-velocity", "outputs"]
+ph = D[:, ::64, 8:21]  # [steps, waves, 13]
 slow = ph[np.arange(steps), wave.argmax(1)]  # the slowest wave of each step
 print("phase cycles: mean wave vs slowest wave of each step (mean over steps)")
 for k, nm in enumerate(PH):
