@@ -336,16 +336,21 @@ HK_DEV bool pair_far_collide(const Arena &w, int p, const CoreBoxes *cb = nullpt
   const float dx = cA.x - cB.x, dy = cA.y - cB.y;
   return dx * dx + dy * dy > lim * lim;
 }
-// b2TimeOfImpact can only report TOUCHING when the GJK core distance falls below target + tolerance
-// (< rA + rB) at some t.  B's core stays within rcore of its COM, which moves on the segment c0 -> c, so the
-// box gap between that swept disc's AABB and A's core AABB bounds the core distance from below: a gap above
-// rA + rB (+ margin) means alpha = 1 exactly, without running the iteration.
+// b2TimeOfImpact can only report TOUCHING when the GJK core distance falls below target + tolerance at
+// some t.  B's core stays within rcore of its COM, which moves on the segment c0 -> c, so the box gap between
+// that swept disc's AABB and A's core AABB bounds the core distance from below: a gap above target +
+// tolerance (+ kToiMargin) means alpha = 1 exactly, without running the iteration.
 // For a player the second stage bounds its core by the exact box at the end-of-sweep rotation q = rot(a)
 // (the transform is synchronised with the sweep whenever the scan runs), widened by rcore * |a - a0|:
 // a core point moves at most that far as the angle runs over [a0, a].
 HK_DEV bool pair_far_toi(const Arena &w, int p, const CoreBoxes &cb) {  // static A, dynamic B, sweeps aligned
   const int fA = SC.pairA[p], fB = SC.pairB[p], bB = SC.pbodyB[p];
-  const float reach = SC.fx[fA].radius + SC.fx[fB].radius + kFarMargin;
+  // b2TimeOfImpact returns TOUCHING only at a t where the core distance (GJK, or a separation function
+  // bounded below by it) is under target + tolerance, target = max(linearSlop, rA + rB - 3 linearSlop),
+  // tolerance = linearSlop / 4; every other outcome maps to alpha 1.  A lower bound on the distance above
+  // that threshold (+ kToiMargin for rounding) therefore gives alpha 1 exactly.
+  const float total = SC.fx[fA].radius + SC.fx[fB].radius;
+  const float reach = fmaxf(kLinearSlop, total - 3.0f * kLinearSlop) + 0.25f * kLinearSlop + kToiMargin;
   const float r = SC.rcore[bB];
   const float c0x = pick(w.d.c0x, bB, 0.0f), c0y = pick(w.d.c0y, bB, 0.0f);
   const float cx = pick(w.d.cx, bB, 0.0f), cy = pick(w.d.cy, bB, 0.0f);
