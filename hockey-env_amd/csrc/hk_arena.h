@@ -710,7 +710,8 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
   w.toiflag = 0u;
   w.cisl = 0u;
   w.bisl = 0u;
-  uint32_t below = 0u;  // pairs whose cached TOI alpha (LDS) is < 1
+  uint32_t below = 0u;      // pairs whose cached TOI alpha (LDS) is < 1
+  uint32_t exhausted = 0u;  // pairs past b2_maxSubSteps TOI events this step (toi_count > 8, kept in LDS)
   for (;;) {
     HK_TIC(T, 5);  // diagnostics: events / min selection -> "toi-events"
     // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
@@ -725,7 +726,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
       const uint32_t bit = 1u << p;
       if (!(w.enabled & bit)) continue;
-      if (LDS(w, kLdsCnt + p) > (float)kMaxSubSteps) continue;
+      if (exhausted & bit) continue;  // c->m_toiCount > b2_maxSubSteps
       if (w.toiflag & bit) {
         elig |= bit;
         continue;
@@ -775,7 +776,9 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     pair_update(w, minc);
     HK_TIC(T, 8);  // diagnostics: TOI event advance + contact update
     w.toiflag &= ~mbit;
-    LDS(w, kLdsCnt + minc) += 1.0f;
+    const float cnt = LDS(w, kLdsCnt + minc) + 1.0f;
+    LDS(w, kLdsCnt + minc) = cnt;
+    if (cnt > (float)kMaxSubSteps) exhausted |= mbit;
     if (!(w.enabled & mbit) || !(w.touch & mbit)) {
       w.enabled &= ~mbit;
       body_set_sweep(w, bA, backA);
