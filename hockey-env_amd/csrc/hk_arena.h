@@ -45,6 +45,17 @@ constexpr uint32_t kEdgeMask[3] = {(1u << 8) | (1u << 10) | (0xFFu << 11),   // 
                                    (1u << 9) | (1u << 10) | (0xFFu << 19),   // player2: 9, 10, 19..26
                                    0x3FFu};                                  // puck: 0..9
 constexpr uint32_t kSensorMask = (1u << 6) | (1u << 7);
+// pairs that take part in continuous collision: static A, not a sensor (Box2D: a non-bullet dynamic pair
+// and sensors never get a TOI)
+constexpr uint32_t kToiPairs = 0x7FFFFFFu & ~kSensorMask & ~((1u << 8) | (1u << 9) | (1u << 10));
+constexpr uint32_t pair_mask_of_scene(bool toi) {
+  uint32_t m = 0u;
+  for (int p = 0; p < NP; ++p)
+    if (toi ? (!g_scene.sensor[p] && g_scene.pbodyA[p] >= 3) : g_scene.sensor[p] != 0) m |= 1u << p;
+  return m;
+}
+static_assert(pair_mask_of_scene(true) == kToiPairs && pair_mask_of_scene(false) == kSensorMask,
+              "pair masks follow the compiled scene's pair table");
 
 // LDS per lane: [0,27) TOI alpha per pair, [27,35) static sweep alpha0, [35,62) TOI sub-step count
 constexpr int kLdsToi = 0, kLdsSal0 = 27, kLdsCnt = 35, kLdsPerLane = 62;
@@ -343,23 +354,24 @@ HK_DEV bool pair_far_collide(const Arena &w, int p, const CoreBoxes *cb = nullpt
 // For a player the second stage bounds its core by the exact box at the end-of-sweep rotation q = rot(a)
 // (the transform is synchronised with the sweep whenever the scan runs), widened by rcore * |a - a0|:
 // a core point moves at most that far as the angle runs over [a0, a].
-HK_DEV bool pair_far_toi(const Arena &w, int p, const CoreBoxes &cb) {  // static A, dynamic B, sweeps aligned
-  const int fA = SC.pairA[p], fB = SC.pairB[p], bB = SC.pbodyB[p];
+// S: SC for a wave-uniform p (first scan pass), SLDS for a per-lane p (later passes)
+HK_DEV bool pair_far_toi(const Arena &w, int p, const CoreBoxes &cb, const Scene &S = SC) {  // static A, dynamic B
+  const int fA = S.pairA[p], fB = S.pairB[p], bB = S.pbodyB[p];
   // b2TimeOfImpact returns TOUCHING only at a t where the core distance (GJK, or a separation function
   // bounded below by it) is under target + tolerance, target = max(linearSlop, rA + rB - 3 linearSlop),
   // tolerance = linearSlop / 4; every other outcome maps to alpha 1.  A lower bound on the distance above
   // that threshold (+ kToiMargin for rounding) therefore gives alpha 1 exactly.
-  const float total = SC.fx[fA].radius + SC.fx[fB].radius;
+  const float total = S.fx[fA].radius + S.fx[fB].radius;
   const float reach = fmaxf(kLinearSlop, total - 3.0f * kLinearSlop) + 0.25f * kLinearSlop + kToiMargin;
-  const float r = SC.rcore[bB];
+  const float r = S.rcore[bB];
   const float c0x = pick(w.d.c0x, bB, 0.0f), c0y = pick(w.d.c0y, bB, 0.0f);
   const float cx = pick(w.d.cx, bB, 0.0f), cy = pick(w.d.cy, bB, 0.0f);
   const float lx = fminf(c0x, cx), ly = fminf(c0y, cy), hx = fmaxf(c0x, cx), hy = fmaxf(c0y, cy);
-  if (box_gap(lx - r, ly - r, hx + r, hy + r, SC.fx_aabb[fA]) > reach) return true;
+  if (box_gap(lx - r, ly - r, hx + r, hy + r, S.fx_aabb[fA]) > reach) return true;
   if (bB == B_PK) return false;  // circle: exact already
   const float(&e)[4] = cb.e[bB == B_P2 ? 1 : 0];
   const float rot = r * fabsf(pick(w.d.a, bB, 0.0f) - pick(w.d.a0, bB, 0.0f));
-  return box_gap(lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot, SC.fx_aabb[fA]) > reach;
+  return box_gap(lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot, S.fx_aabb[fA]) > reach;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -712,6 +724,8 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
   w.bisl = 0u;
   uint32_t below = 0u;      // pairs whose cached TOI alpha (LDS) is < 1
   uint32_t exhausted = 0u;  // pairs past b2_maxSubSteps TOI events this step (toi_count > 8, kept in LDS)
+  uint32_t redo = 0u;       // pairs a later scan pass must visit: the last event's body's contacts
+  bool first = true;
   for (;;) {
     HK_TIC(T, 5);  // diagnostics: events / min selection -> "toi-events"
     // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
@@ -723,7 +737,37 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     uint32_t elig = 0u, pending = 0u;
     CoreBoxes cb;  // the players' poses are fixed during the pass (only sweep starts move)
     core_boxes(w, cb);
-    for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
+    if (!first) {
+      // Later passes: an event re-enables TOI only on the moved dynamic body's contacts (their flags were
+      // cleared).  Every other pair keeps its eligibility and cached alpha (cached pairs are eligible;
+      // the rest were skipped for reasons no event changes), so only `redo` is visited, in pair order.
+      elig = w.toiflag & w.enabled & ~exhausted;
+      uint32_t todo = redo & kToiPairs & w.enabled & ~exhausted & ~w.toiflag;
+      while (todo) {
+        const int p = __ffs(todo) - 1;
+        todo &= todo - 1u;
+        const uint32_t bit = 1u << p;
+        const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
+        if (!pick(w.d.awake, bB, 0)) continue;
+        elig |= bit;
+        w.toiflag |= bit;
+        const float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
+        if (a0A < a0B) {
+          LDS(w, kLdsSal0 + bA - 3) = a0B;
+        } else if (a0B < a0A) {
+          toi_drain(w, pending, below);
+          Sweep sw = body_sweep(w, bB);
+          sweep_advance(sw, a0A);
+          body_set_sweep(w, bB, sw);
+        }
+        if (pair_far_toi(w, p, cb, SLDS)) {
+          below &= ~bit;
+        } else {
+          pending |= bit;
+        }
+      }
+    }
+    for (int p = 0; p < NP && first; ++p) {  // first pass, uniform: scene data through scalar loads
       const uint32_t bit = 1u << p;
       if (!(w.enabled & bit)) continue;
       if (exhausted & bit) continue;  // c->m_toiCount > b2_maxSubSteps
@@ -752,6 +796,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
         pending |= bit;
       }
     }
+    first = false;
     HK_TIC(T, 6);  // diagnostics: scan pass -> "toi-scan"
     // (2) per-lane queue: every lane runs b2TimeOfImpact on its own next pair (lanes stay converged on
     //     the same code instead of serialising over the union of the wave's pairs)
@@ -785,6 +830,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
       body_set_sweep(w, bB, backB);
       sync_xf(w, bA);
       sync_xf(w, bB);
+      redo = 0u;  // sweeps restored: every other pair's flag and alpha stand
       continue;
     }
     w.n_toi++;
@@ -830,6 +876,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     const uint32_t em = pick(kEdgeMask, bB, 0u);
     w.toiflag &= ~em;
     w.cisl &= ~em;
+    redo = em;
   }
 }
 
