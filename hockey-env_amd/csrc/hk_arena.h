@@ -374,6 +374,51 @@ HK_DEV bool pair_far_toi(const Arena &w, int p, const CoreBoxes &cb, const Scene
   return box_gap(lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot, S.fx_aabb[fA]) > reach;
 }
 
+// First-pass bulk settlement of the TOI scan (solve_toi).  A dynamic body whose swept core box lies inside its
+// interior rectangle is farther than the TOI reach from each of its static fixtures (walls bound the
+// rectangle in y, posts and goals in x), so pair_far_toi holds for all of its TOI pairs.  The rectangles are
+// compile-time (1 mm inside the exact bound); the static_asserts re-check every fixture against them.
+struct Rect { float x0, y0, x1, y1; };
+constexpr float cmax(float a, float b) { return a > b ? a : b; }
+constexpr float cmin(float a, float b) { return a < b ? a : b; }
+constexpr float toi_reach(int fB) {
+  const float total = g_scene.fx[F_WT].radius + g_scene.fx[fB].radius;
+  return cmax(kLinearSlop, total - 3.0f * kLinearSlop) + 0.25f * kLinearSlop + kToiMargin;
+}
+constexpr Rect interior_rect(int fB, bool goals) {
+  const float e = toi_reach(fB) + 1e-3f;
+  float xl = cmax(g_scene.fx_aabb[F_PLT][2], g_scene.fx_aabb[F_PLB][2]);
+  float xr = cmin(g_scene.fx_aabb[F_PRT][0], g_scene.fx_aabb[F_PRB][0]);
+  if (goals) {
+    xl = cmax(xl, g_scene.fx_aabb[F_G1][2]);
+    xr = cmin(xr, g_scene.fx_aabb[F_G2][0]);
+  }
+  return Rect{xl + e, g_scene.fx_aabb[F_WB][3] + e, xr - e, g_scene.fx_aabb[F_WT][1] - e};
+}
+constexpr Rect kInteriorPuck = interior_rect(F_PK, false), kInteriorPlayer = interior_rect(F_P1, true);
+constexpr bool rect_clear(const Rect &r, int f, float reach) {
+  const float *b = g_scene.fx_aabb[f];
+  return cmax(cmax(b[0] - r.x1, r.x0 - b[2]), cmax(b[1] - r.y1, r.y0 - b[3])) > reach;
+}
+constexpr bool interior_ok() {
+  const int fs[8] = {F_WT, F_WB, F_PLT, F_PLB, F_PRT, F_PRB, F_G1, F_G2};
+  bool ok = g_scene.fx[F_P1].radius == g_scene.fx[F_P2].radius;
+  for (int k = 0; k < 8; ++k) ok = ok && rect_clear(kInteriorPlayer, fs[k], toi_reach(F_P1));
+  for (int k = 0; k < 6; ++k) ok = ok && rect_clear(kInteriorPuck, fs[k], toi_reach(F_PK));
+  for (int p = 0; p < NP; ++p)  // the puck's TOI pairs are 0..5, the players' their static pairs (kEdgeMask)
+    if ((kToiPairs >> p) & 1u) {
+      const int f = g_scene.pairA[p];
+      const bool known = f == F_WT || f == F_WB || f == F_PLT || f == F_PLB || f == F_PRT || f == F_PRB ||
+                         (g_scene.pbodyB[p] != B_PK && (f == F_G1 || f == F_G2));
+      ok = ok && known;
+    }
+  return ok;
+}
+static_assert(interior_ok(), "interior rectangles clear every static fixture of a TOI pair by the TOI reach");
+HK_DEV bool inside(const Rect &r, float lx, float ly, float hx, float hy) {
+  return lx > r.x0 && ly > r.y0 && hx < r.x1 && hy < r.y1;
+}
+
 // ------------------------------------------------------------------------------------------------
 // ContactDetector.BeginContact (hockey_env.py:44-76) and b2Contact::Update
 // ------------------------------------------------------------------------------------------------
@@ -737,48 +782,45 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     uint32_t elig = 0u, pending = 0u;
     CoreBoxes cb;  // the players' poses are fixed during the pass (only sweep starts move)
     core_boxes(w, cb);
-    if (!first) {
+    uint32_t todo;
+    if (first) {
+      uint32_t settled = 0u;
+      // The first pass has no order-dependent side effect (every alpha0 is still 0, so the alignment is a
+      // no-op): the TOI pairs of a body inside its interior rectangle are settled in bulk as eligible with
+      // alpha 1, exactly what the per-pair pass below would record for them.
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const float lx = fminf(w.d.c0x[b], w.d.cx[b]), ly = fminf(w.d.c0y[b], w.d.cy[b]);
+        const float hx = fmaxf(w.d.c0x[b], w.d.cx[b]), hy = fmaxf(w.d.c0y[b], w.d.cy[b]);
+        bool in;
+        if (b == B_PK) {
+          in = inside(kInteriorPuck, lx, ly, hx, hy);  // a circle's core is its centre
+        } else {
+          const float(&e)[4] = cb.e[b];
+          const float rot = SC.rcore[b] * fabsf(w.d.a[b] - w.d.a0[b]);
+          in = inside(kInteriorPlayer, lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot);
+        }
+        if (in && w.d.awake[b]) settled |= kEdgeMask[b];
+      }
+      settled &= kToiPairs & w.enabled;
+      elig |= settled;
+      w.toiflag |= settled;
+      below &= ~settled;
+      todo = kToiPairs & w.enabled & ~settled;
+    } else {
       // Later passes: an event re-enables TOI only on the moved dynamic body's contacts (their flags were
       // cleared).  Every other pair keeps its eligibility and cached alpha (cached pairs are eligible;
-      // the rest were skipped for reasons no event changes), so only `redo` is visited, in pair order.
+      // the rest were skipped for reasons no event changes), so only `redo` is visited.
       elig = w.toiflag & w.enabled & ~exhausted;
-      uint32_t todo = redo & kToiPairs & w.enabled & ~exhausted & ~w.toiflag;
-      while (todo) {
-        const int p = __ffs(todo) - 1;
-        todo &= todo - 1u;
-        const uint32_t bit = 1u << p;
-        const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
-        if (!pick(w.d.awake, bB, 0)) continue;
-        elig |= bit;
-        w.toiflag |= bit;
-        const float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
-        if (a0A < a0B) {
-          LDS(w, kLdsSal0 + bA - 3) = a0B;
-        } else if (a0B < a0A) {
-          toi_drain(w, pending, below);
-          Sweep sw = body_sweep(w, bB);
-          sweep_advance(sw, a0A);
-          body_set_sweep(w, bB, sw);
-        }
-        if (pair_far_toi(w, p, cb, SLDS)) {
-          below &= ~bit;
-        } else {
-          pending |= bit;
-        }
-      }
+      todo = redo & kToiPairs & w.enabled & ~exhausted & ~w.toiflag;
     }
-    for (int p = 0; p < NP && first; ++p) {  // first pass, uniform: scene data through scalar loads
+    // in pair order, per lane: eligibility, sweep alignment and the far test of the pairs still open
+    while (todo) {
+      const int p = __ffs(todo) - 1;
+      todo &= todo - 1u;
       const uint32_t bit = 1u << p;
-      if (!(w.enabled & bit)) continue;
-      if (exhausted & bit) continue;  // c->m_toiCount > b2_maxSubSteps
-      if (w.toiflag & bit) {
-        elig |= bit;
-        continue;
-      }
-      if (SC.sensor[p]) continue;
-      const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
-      if (bA < 3) continue;                   // dynamic-dynamic, non-bullet: no continuous collision
-      if (!pick(w.d.awake, bB, 0)) continue;  // static A is never active
+      const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
+      if (!pick(w.d.awake, bB, 0)) continue;
       elig |= bit;
       w.toiflag |= bit;
       const float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
@@ -790,8 +832,8 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
         sweep_advance(sw, a0A);
         body_set_sweep(w, bB, sw);
       }
-      if (pair_far_toi(w, p, cb)) {
-        below &= ~bit;  // alpha 1
+      if (pair_far_toi(w, p, cb, SLDS)) {
+        below &= ~bit;
       } else {
         pending |= bit;
       }
