@@ -290,9 +290,9 @@ HK_DEV void apply_torque(Arena &w, float t) {
 
 // ------------------------------------------------------------------------------------------------
 // lane-local broad phase (exact outcome-preserving rejection)
-//   Box2D clipping emits points up to sqrt(2) * totalRadius from the reference polygon and the circle
-//   manifold up to totalRadius: reach = 2 * (rA + rB); every TOI "touching" exit needs the core
-//   distance below target + tol < rA + rB at some t.
+//   Box2D clipping emits points up to sqrt(2) * totalRadius from the reference polygon: reach = 2 * (rA + rB)
+//   for polygon pairs; b2CollidePolygonAndCircle and b2TestOverlap need the core distance within rA + rB;
+//   every TOI "touching" exit needs the core distance below target + tol < rA + rB at some t.
 // ------------------------------------------------------------------------------------------------
 HK_DEV float box_gap(float ax0, float ay0, float ax1, float ay1, const float *b) {
   return fmaxf(fmaxf(b[0] - ax1, ax0 - b[2]), fmaxf(b[1] - ay1, ay0 - b[3]));
@@ -331,7 +331,11 @@ HK_DEV bool static_far_collide(const Scene &S, int fA, int bB, v2 cB, const floa
 // S: SC for a wave-uniform p (pair-table loops), SLDS for a per-lane p
 HK_DEV bool pair_far_collide(const Arena &w, int p, const CoreBoxes *cb = nullptr, const Scene &S = SC) {
   const int fA = S.pairA[p], fB = S.pairB[p], bA = S.pbodyA[p], bB = S.pbodyB[p];
-  const float reach = 2.0f * (S.fx[fA].radius + S.fx[fB].radius) + kFarMargin;
+  // A polygon-circle manifold (and a sensor overlap) needs the circle centre within the total radius of
+  // the polygon core, so a circle pair is far beyond total + rounding margin; polygon pairs keep the
+  // clipping bound 2 * total (+ kFarMargin).
+  const float total = S.fx[fA].radius + S.fx[fB].radius;
+  const float reach = S.fx[fB].circle ? total + kToiMargin : 2.0f * total + kFarMargin;
   const v2 cB = body_c(w, bB);
   const float rB = S.rcore[bB];
   if (bA >= 3) {

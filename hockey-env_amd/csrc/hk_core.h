@@ -72,8 +72,8 @@ struct Scene {
 
 // margin of the conservative rejection tests: covers float rounding of transforms / sweep interpolation
 constexpr float kFarMargin = 0.05f;
-// margin of the b2TimeOfImpact rejection (hk_arena.h pair_far_toi): covers the float rounding of sweep
-// interpolation and GJK distances (~1e-5 m here), two orders of magnitude below it
+// margin of the exact distance rejections (hk_arena.h pair_far_toi, circle pairs of pair_far_collide): covers
+// the float rounding of sweep interpolation, transforms and GJK distances (~1e-5 m here), far below it
 constexpr float kToiMargin = 0.005f;
 
 // ---------------------------------------------------------------------------------------------
