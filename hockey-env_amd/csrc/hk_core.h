@@ -70,8 +70,9 @@ struct Scene {
   float rcore[3];         // max distance from a dynamic body's COM to its core (radius-free) shape
 };
 
-// margin of the conservative rejection tests: covers float rounding of transforms / sweep interpolation
-constexpr float kFarMargin = 0.05f;
+// rounding margin of the polygon-pair rejection (2 x total radius, hk_arena.h pair_far_collide): contacts use
+// at most ~1.4 x total radius (tests/test_broadphase_bound.py), float rounding ~1e-5 m
+constexpr float kFarMargin = 0.005f;
 // margin of the exact distance rejections (hk_arena.h pair_far_toi, circle pairs of pair_far_collide): covers
 // the float rounding of sweep interpolation, transforms and GJK distances (~1e-5 m here), far below it
 constexpr float kToiMargin = 0.005f;
