@@ -116,6 +116,8 @@ HK_DEV f2 bc(float s) { return f2{s, s}; }
 HK_DEV f2 perp(f2 r) { return f2{-r[1], r[0]}; }
 HK_DEV float pdot(f2 a, f2 b) { const f2 p = a * b; return p[0] + p[1]; }                // dot()
 HK_DEV float pcrs(f2 a, f2 b) { const f2 p = a * f2{b[1], b[0]}; return p[0] - p[1]; }  // crs()
+// mul_rv(q, v) == (c x + s (-y), c y + s x): a + (-b) == a - b and + commutes, bit for bit
+HK_DEV f2 prv(rot q, f2 v) { return bc(q.c) * v + bc(q.s) * perp(v); }
 
 HK_DEV float fmin2(float a, float b) { return a < b ? a : b; }
 HK_DEV float fmax2(float a, float b) { return a > b ? a : b; }

@@ -401,61 +401,63 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
 
 // one NGS position pass over one contact (b2ContactSolver::SolvePositionConstraints body).  In this scene
 // SolveTOIPositionConstraints' mass gating is the identity (see solve_toi), so one routine serves both.
+// The 2-vector arithmetic is packed (f2): the same float operations in the same order as the scalar form.
 HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float minSep, const ManGeo &m) {
   Dyn &B = w.d;
   const float mA = s.mA, mB = s.mB, iA = s.iA, iB = s.iB;
   const int bA = fs_bA(s), bB = fs_bB(s), pcount = fs_pcount(s);
-  const v2 lcA = local_center(bA), lcB = local_center(bB);
+  const f2 lcA = F2(local_center(bA)), lcB = F2(local_center(bB));
   const float rAr = pair_rA(), rBr = pair_rB(bB);
-  v2 cA, cB;
+  v2 cA0, cB0;
   float aA, aB;
-  get_pos(B, bA, cA, aA);
-  get_pos(B, bB, cB, aB);
+  get_pos(B, bA, cA0, aA);
+  get_pos(B, bB, cB0, aB);
+  f2 cA = F2(cA0), cB = F2(cB0);
+  const f2 ln = F2(m.ln), lp = F2(m.lp);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (j < pcount) {
-      xform xA, xB;
+      rot qA, qB;
       // a static body stays at angle +0 (iA == 0 keeps aA bit-exact), and rot_set(+0) == (+0, 1)
       if (bA >= 3) {
-        xA.q.s = 0.0f;
-        xA.q.c = 1.0f;
+        qA.s = 0.0f;
+        qA.c = 1.0f;
       } else {
-        xA.q = rot_set(aA);
+        qA = rot_set(aA);
       }
-      xB.q = rot_set(aB);
-      xA.p = vsub(cA, mul_rv(xA.q, lcA));
-      xB.p = vsub(cB, mul_rv(xB.q, lcB));
-      v2 normal, point;
+      qB = rot_set(aB);
+      const f2 pA = cA - prv(qA, lcA), pB = cB - prv(qB, lcB);
+      f2 normal, point;
       float sep;
       if (m.type == 1) {
-        normal = mul_rv(xA.q, m.ln);
-        v2 plane = mul_xv(xA, m.lp);
-        v2 clip = mul_xv(xB, m.pt[j]);
-        sep = dot(vsub(clip, plane), normal) - rAr - rBr;
+        normal = prv(qA, ln);
+        const f2 plane = prv(qA, lp) + pA;
+        const f2 clip = prv(qB, F2(m.pt[j])) + pB;
+        sep = pdot(clip - plane, normal) - rAr - rBr;
         point = clip;
       } else {
-        normal = mul_rv(xB.q, m.ln);
-        v2 plane = mul_xv(xB, m.lp);
-        v2 clip = mul_xv(xA, m.pt[j]);
-        sep = dot(vsub(clip, plane), normal) - rAr - rBr;
+        normal = prv(qB, ln);
+        const f2 plane = prv(qB, lp) + pB;
+        const f2 clip = prv(qA, F2(m.pt[j])) + pA;
+        sep = pdot(clip - plane, normal) - rAr - rBr;
         point = clip;
-        normal = vneg(normal);
+        normal = -normal;
       }
-      v2 rA = vsub(point, cA), rB = vsub(point, cB);
+      const f2 rA = point - cA, rB = point - cB;
       minSep = fmin2(minSep, sep);
       float C = fclamp(baum * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-      float rnA = crs(rA, normal), rnB = crs(rB, normal);
+      float rnA = pcrs(rA, normal), rnB = pcrs(rB, normal);
       float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
       float impulse = K > 0.0f ? -C / K : 0.0f;
-      v2 Pv = vs(impulse, normal);
-      cA = vsub(cA, vs(mA, Pv));
-      aA -= iA * crs(rA, Pv);
-      cB = vadd(cB, vs(mB, Pv));
-      aB += iB * crs(rB, Pv);
+      const f2 P = bc(impulse) * normal;
+      cA = cA - bc(mA) * P;
+      aA -= iA * pcrs(rA, P);
+      cB = cB + bc(mB) * P;
+      aB += iB * pcrs(rB, P);
     }
   }
-  if (bA < 3) set_pos(B, bA, cA, aA);
-  set_pos(B, bB, cB, aB);
+  if (bA < 3) set_pos(B, bA, V2(cA), aA);
+  set_pos(B, bB, V2(cB), aB);
   return minSep;
 }
 
