@@ -232,6 +232,14 @@ HK_DEV double hk_cos(double x) {
   }
 }
 
+// true if the predicate holds on any active lane of the wave (a wave-uniform decision).  The host harness
+// runs one lane at a time, where it is the lane's own predicate.
+#if defined(__HIP_DEVICE_COMPILE__)
+HK_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
+#else
+HK_DEV bool wave_any(bool p) { return p; }
+#endif
+
 // Analysis build only (-DHK_ASM_MARKS): labels in the device assembly around hot regions.
 #ifdef HK_ASM_MARKS
 #define HK_MARK(x) asm volatile(";HKMARK " #x)

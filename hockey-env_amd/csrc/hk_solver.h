@@ -480,7 +480,8 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
 template <int C>
 struct RegSlots {
   static constexpr bool kRegister = true;
-  static constexpr bool kOneFast = (C == kToiC);  // the TOI mini-island solve (islands: register budget)
+  static constexpr bool kOneFast = true;  // one-contact solves keep the two bodies' velocities in locals
+  static constexpr bool kWaveGated = (C != kToiC);  // islands: only in waves without larger islands
   FSlot s[C];
   ManGeo g[C];  // position-phase geometry, loaded once per position loop (load_geo)
   HK_DEV void load_geo(int nc, const Arena &w) {
@@ -504,6 +505,7 @@ struct RegSlots {
 struct HbmSlots {
   static constexpr bool kRegister = false;
   static constexpr bool kOneFast = false;
+  static constexpr bool kWaveGated = false;
   float *ws;
   int64_t n, a;
   HK_DEV float &word(int i, int k) const { return ws[((int64_t)i * kSlotWords + k) * n + a]; }
@@ -579,7 +581,14 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
 template <typename SL>
 HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
   if constexpr (SL::kRegister && SL::kOneFast) {
-    if (nc == 1) return velocity_iterations_one(S.s[0], B);
+    if constexpr (SL::kWaveGated) {
+      // island solves: the one-contact loop only when no active lane of the wave solves a larger island,
+      // so a wave never runs both loops one after the other (which would lengthen the slowest waves)
+      const bool multi = wave_any(nc > 1);
+      if (nc == 1 && !multi) return velocity_iterations_one(S.s[0], B);
+    } else {
+      if (nc == 1) return velocity_iterations_one(S.s[0], B);
+    }
   }
   uint32_t sb[9];
 #pragma unroll
