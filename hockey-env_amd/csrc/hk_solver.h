@@ -221,91 +221,9 @@ HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
   set_vel(B, bB, vB, wB);
 }
 
-// one b2ContactSolver::SolveVelocityConstraints pass over one contact
-// the body-velocity-local form: vA, wA, vB, wB are the two bodies' velocities, updated in place
-HK_DEV void fslot_solve_velocity_v(FSlot &s, v2 &vA, float &wA, v2 &vB, float &wB) {
-  const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
-  const int vcount = fs_vcount(s);
-  const v2 normal = V(s.nx, s.ny), tangent = crs_vs(normal, 1.0f);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (j < vcount) {
-      const v2 rA = V(s.rAx[j], s.rAy[j]), rB = V(s.rBx[j], s.rBy[j]);
-      v2 dv = vsub(vsub(vadd(vB, crs_sv(wB, rB)), vA), crs_sv(wA, rA));
-      float vt = dot(dv, tangent) - 0.0f;
-      float lambda = s.tm[j] * (-vt);
-      float maxF = s.fr * s.ni[j];
-      float newI = fclamp(s.ti[j] + lambda, -maxF, maxF);
-      lambda = newI - s.ti[j];
-      s.ti[j] = newI;
-      v2 P = vs(lambda, tangent);
-      vA = vsub(vA, vs(mA, P));
-      wA -= iA * crs(rA, P);
-      vB = vadd(vB, vs(mB, P));
-      wB += iB * crs(rB, P);
-    }
-  }
-  if (vcount == 1) {
-    const v2 rA = V(s.rAx[0], s.rAy[0]), rB = V(s.rBx[0], s.rBy[0]);
-    v2 dv = vsub(vsub(vadd(vB, crs_sv(wB, rB)), vA), crs_sv(wA, rA));
-    float vn = dot(dv, normal);
-    float lambda = -s.nm[0] * (vn - s.bias[0]);
-    float newI = fmax2(s.ni[0] + lambda, 0.0f);
-    lambda = newI - s.ni[0];
-    s.ni[0] = newI;
-    v2 P = vs(lambda, normal);
-    vA = vsub(vA, vs(mA, P));
-    wA -= iA * crs(rA, P);
-    vB = vadd(vB, vs(mB, P));
-    wB += iB * crs(rB, P);
-  } else {
-    const v2 r1A = V(s.rAx[0], s.rAy[0]), r1B = V(s.rBx[0], s.rBy[0]);
-    const v2 r2A = V(s.rAx[1], s.rAy[1]), r2B = V(s.rBx[1], s.rBy[1]);
-    v2 a = V(s.ni[0], s.ni[1]);
-    v2 dv1 = vsub(vsub(vadd(vB, crs_sv(wB, r1B)), vA), crs_sv(wA, r1A));
-    v2 dv2 = vsub(vsub(vadd(vB, crs_sv(wB, r2B)), vA), crs_sv(wA, r2A));
-    float vn1 = dot(dv1, normal), vn2 = dot(dv2, normal);
-    v2 b;
-    b.x = vn1 - s.bias[0];
-    b.y = vn2 - s.bias[1];
-    b = vsub(b, V(s.Kxx * a.x + s.Kxy * a.y, s.Kxy * a.x + s.Kyy * a.y));
-    v2 x = vneg(V(s.Nxx * b.x + s.Nxy * b.y, s.Nxy * b.x + s.Nyy * b.y));
-    int ok = 0;
-    if (x.x >= 0.0f && x.y >= 0.0f) ok = 1;
-    if (!ok) {
-      x.x = -s.nm[0] * b.x;
-      x.y = 0.0f;
-      vn2 = s.Kxy * x.x + b.y;
-      if (x.x >= 0.0f && vn2 >= 0.0f) ok = 1;
-    }
-    if (!ok) {
-      x.x = 0.0f;
-      x.y = -s.nm[1] * b.y;
-      vn1 = s.Kxy * x.y + b.x;
-      if (x.y >= 0.0f && vn1 >= 0.0f) ok = 1;
-    }
-    if (!ok) {
-      x.x = 0.0f;
-      x.y = 0.0f;
-      vn1 = b.x;
-      vn2 = b.y;
-      if (vn1 >= 0.0f && vn2 >= 0.0f) ok = 1;
-    }
-    if (ok) {
-      v2 d = vsub(x, a);
-      v2 P1 = vs(d.x, normal), P2 = vs(d.y, normal);
-      vA = vsub(vA, vs(mA, vadd(P1, P2)));
-      wA -= iA * (crs(r1A, P1) + crs(r2A, P2));
-      vB = vadd(vB, vs(mB, vadd(P1, P2)));
-      wB += iB * (crs(r1B, P1) + crs(r2B, P2));
-      s.ni[0] = x.x;
-      s.ni[1] = x.y;
-    }
-  }
-}
-
-// fslot_solve_velocity_v on packed body velocities: the same float operations in the same order, with the
-// 2-vector arithmetic issued as packed fp32 instructions
+// one b2ContactSolver::SolveVelocityConstraints pass over one contact (tangent rows, then the normal row or the
+// 2-point block solver), on the two bodies' velocities held in locals; the 2-vector arithmetic is packed fp32
+// (f2) with Box2D's float operations in Box2D's order
 HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &wB) {
   const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
   const int vcount = fs_vcount(s);
