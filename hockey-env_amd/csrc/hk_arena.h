@@ -141,6 +141,34 @@ HK_DEV void place(T (&x)[3], int b, T v) {
   x[1] = (b == 1) ? v : x1;
   x[2] = (b == 2) ? v : x2;
 }
+// Pair sides (build_scene): body A is player 1, player 2 or a static body, never the puck; body B is a
+// dynamic body.  The side-specific selects drop the comparisons that can never hold (velocity-loop VALU).
+constexpr bool pair_sides_ok() {
+  for (int p = 0; p < NP; ++p)
+    if (g_scene.pbodyA[p] == B_PK || g_scene.pbodyB[p] > B_PK) return false;
+  return true;
+}
+static_assert(pair_sides_ok(), "pair body A is never the puck, pair body B is always dynamic");
+template <typename T>
+HK_DEV T pick_a(const T (&x)[3], int b, T dflt) {
+  const T x0 = x[0], x1 = x[1];
+  T r = (b == 1) ? x1 : dflt;
+  r = (b == 0) ? x0 : r;
+  return r;
+}
+template <typename T>
+HK_DEV T pick_b(const T (&x)[3], int b) {
+  const T x0 = x[0], x1 = x[1], x2 = x[2];
+  T r = (b == 1) ? x1 : x2;
+  r = (b == 0) ? x0 : r;
+  return r;
+}
+template <typename T>
+HK_DEV void place_a(T (&x)[3], int b, T v) {
+  const T x0 = x[0], x1 = x[1];
+  x[0] = (b == 0) ? v : x0;
+  x[1] = (b == 1) ? v : x1;
+}
 HK_DEV float &LDS(Arena &w, int k) { return w.lds[k * 64 + w.lane]; }
 // Box2D manifold record of solid-pair slot `slot` for this arena: [slot][arena][16 words].  A lane's
 // record is one 64-B block, so the per-lane (divergent) slot accesses of the near-pair / island / TOI

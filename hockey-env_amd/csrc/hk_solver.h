@@ -35,26 +35,45 @@ HK_DEV int fs_vcount(const FSlot &s) { return (s.bits >> 15) & 3; }
 HK_DEV int fs_pcount(const FSlot &s) { return (s.bits >> 17) & 3; }
 HK_DEV int fs_type(const FSlot &s) { return (s.bits >> 19) & 3; }
 
-HK_DEV void get_vel(const Dyn &B, int b, v2 &v, float &w) {
-  v = V(pick(B.vx, b, 0.0f), pick(B.vy, b, 0.0f));
-  w = pick(B.w, b, 0.0f);
+// body access by pair side (pick_a / pick_b / place_a: body A is never the puck, body B is dynamic)
+HK_DEV void get_vel_a(const Dyn &B, int b, v2 &v, float &w) {
+  v = V(pick_a(B.vx, b, 0.0f), pick_a(B.vy, b, 0.0f));
+  w = pick_a(B.w, b, 0.0f);
 }
-HK_DEV void set_vel(Dyn &B, int b, v2 v, float w) {
+HK_DEV void get_vel_b(const Dyn &B, int b, v2 &v, float &w) {
+  v = V(pick_b(B.vx, b), pick_b(B.vy, b));
+  w = pick_b(B.w, b);
+}
+HK_DEV void set_vel_a(Dyn &B, int b, v2 v, float w) {
+  place_a(B.vx, b, v.x);
+  place_a(B.vy, b, v.y);
+  place_a(B.w, b, w);
+}
+HK_DEV void set_vel_b(Dyn &B, int b, v2 v, float w) {
   place(B.vx, b, v.x);
   place(B.vy, b, v.y);
   place(B.w, b, w);
 }
 // position of body b (a static body sits at its origin with angle 0)
-HK_DEV void get_pos(const Dyn &B, int b, v2 &c, float &a) {
+HK_DEV void get_pos_a(const Dyn &B, int b, v2 &c, float &a) {
   if (b < 3) {
-    c = V(pick(B.cx, b, 0.0f), pick(B.cy, b, 0.0f));
-    a = pick(B.a, b, 0.0f);
+    c = V(pick_a(B.cx, b, 0.0f), pick_a(B.cy, b, 0.0f));
+    a = pick_a(B.a, b, 0.0f);
   } else {
     c = V(SLDS.spx[b], SLDS.spy[b]);
     a = 0.0f;
   }
 }
-HK_DEV void set_pos(Dyn &B, int b, v2 c, float a) {
+HK_DEV void get_pos_b(const Dyn &B, int b, v2 &c, float &a) {
+  c = V(pick_b(B.cx, b), pick_b(B.cy, b));
+  a = pick_b(B.a, b);
+}
+HK_DEV void set_pos_a(Dyn &B, int b, v2 c, float a) {
+  place_a(B.cx, b, c.x);
+  place_a(B.cy, b, c.y);
+  place_a(B.a, b, a);
+}
+HK_DEV void set_pos_b(Dyn &B, int b, v2 c, float a) {
   place(B.cx, b, c.x);
   place(B.cy, b, c.y);
   place(B.a, b, a);
@@ -118,10 +137,10 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
   const float rAr = pair_rA(), rBr = pair_rB(bB);
   v2 cA, cB, vA, vB;
   float aA, aB, wA, wB;
-  get_pos(B, bA, cA, aA);
-  get_pos(B, bB, cB, aB);
-  get_vel(B, bA, vA, wA);
-  get_vel(B, bB, vB, wB);
+  get_pos_a(B, bA, cA, aA);
+  get_pos_b(B, bB, cB, aB);
+  get_vel_a(B, bA, vA, wA);
+  get_vel_b(B, bB, vB, wB);
   xform xA, xB;
   if (bA >= 3) {  // static body: angle +0, rot_set(+0) == (+0, 1)
     xA.q.s = 0.0f;
@@ -204,8 +223,8 @@ HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s), vcount = fs_vcount(s);
   v2 vA, vB;
   float wA, wB;
-  get_vel(B, bA, vA, wA);
-  get_vel(B, bB, vB, wB);
+  get_vel_a(B, bA, vA, wA);
+  get_vel_b(B, bB, vB, wB);
   const v2 normal = V(s.nx, s.ny), tangent = crs_vs(normal, 1.0f);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -217,8 +236,8 @@ HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
       vB = vadd(vB, vs(s.mB, P));
     }
   }
-  set_vel(B, bA, vA, wA);
-  set_vel(B, bB, vB, wB);
+  set_vel_a(B, bA, vA, wA);
+  set_vel_b(B, bB, vB, wB);
 }
 
 // one b2ContactSolver::SolveVelocityConstraints pass over one contact (tangent rows, then the normal row or the
@@ -309,12 +328,12 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s);
   v2 vA, vB;
   float wA, wB;
-  get_vel(B, bA, vA, wA);
-  get_vel(B, bB, vB, wB);
+  get_vel_a(B, bA, vA, wA);
+  get_vel_b(B, bB, vB, wB);
   f2 pA = F2(vA), pB = F2(vB);
   fslot_solve_velocity_p(s, pA, wA, pB, wB);
-  set_vel(B, bA, V2(pA), wA);
-  set_vel(B, bB, V2(pB), wB);
+  set_vel_a(B, bA, V2(pA), wA);
+  set_vel_b(B, bB, V2(pB), wB);
 }
 
 // one NGS position pass over one contact (b2ContactSolver::SolvePositionConstraints body).  In this scene
@@ -328,8 +347,8 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
   const float rAr = pair_rA(), rBr = pair_rB(bB);
   v2 cA0, cB0;
   float aA, aB;
-  get_pos(B, bA, cA0, aA);
-  get_pos(B, bB, cB0, aB);
+  get_pos_a(B, bA, cA0, aA);
+  get_pos_b(B, bB, cB0, aB);
   f2 cA = F2(cA0), cB = F2(cB0);
   const f2 ln = F2(m.ln), lp = F2(m.lp);
 #pragma unroll
@@ -374,8 +393,8 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
       aB += iB * pcrs(rB, P);
     }
   }
-  if (bA < 3) set_pos(B, bA, V2(cA), aA);
-  set_pos(B, bB, V2(cB), aB);
+  if (bA < 3) set_pos_a(B, bA, V2(cA), aA);
+  set_pos_b(B, bB, V2(cB), aB);
   return minSep;
 }
 
@@ -459,8 +478,8 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
   const bool dynA = bA < 3;
   v2 vA2, vB2;
   float wA, wB;
-  get_vel(B, bA, vA2, wA);
-  get_vel(B, bB, vB2, wB);
+  get_vel_a(B, bA, vA2, wA);
+  get_vel_b(B, bB, vB2, wB);
   f2 vA = F2(vA2), vB = F2(vB2);
   uint32_t sn[10];
 #pragma unroll
@@ -490,8 +509,8 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
     if (it + 3 >= 7 && diff == 0u) active = false;
   }
   HK_MARK(vone_end);
-  if (dynA) set_vel(B, bA, V2(vA), wA);
-  set_vel(B, bB, V2(vB), wB);
+  if (dynA) set_vel_a(B, bA, V2(vA), wA);
+  set_vel_b(B, bB, V2(vB), wB);
   return it;
 }
 
