@@ -417,8 +417,7 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
 template <int C>
 struct RegSlots {
   static constexpr bool kRegister = true;
-  static constexpr bool kOneFast = true;  // one-contact solves keep the two bodies' velocities in locals
-  static constexpr bool kWaveGated = (C != kToiC);  // islands: only in waves without larger islands
+  static_assert(C >= 2, "the one- and two-contact loops use slots 0 and 1");
   FSlot s[C];
   ManGeo g[C];  // position-phase geometry, loaded once per position loop (load_geo)
   HK_DEV void load_geo(int nc, const Arena &w) {
@@ -441,8 +440,6 @@ struct RegSlots {
 
 struct HbmSlots {
   static constexpr bool kRegister = false;
-  static constexpr bool kOneFast = false;
-  static constexpr bool kWaveGated = false;
   float *ws;
   int64_t n, a;
   HK_DEV float &word(int i, int k) const { return ws[((int64_t)i * kSlotWords + k) * n + a]; }
@@ -514,17 +511,99 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
   return it;
 }
 
+// Two-contact solve (waves whose islands all have at most two contacts; a one-contact lane runs it with
+// contact 1 masked off).  Each contact keeps its two bodies' velocities in locals; after a contact is
+// solved, the other contact's copy of any body it shares (equal body index) is refreshed from it, so every
+// solve reads exactly the velocities the body-file loop reads, at 2 selects per shared-body component
+// instead of the body file's gather and scatter.  A static body A is +0 at every solve, as get_vel_a
+// returns it.  The snapshot covers every island body (each appears in some contact) and both contacts'
+// impulses: the set the general loop compares, some bodies twice.
+HK_DEV f2 sel2(bool c, f2 a, f2 b) { return f2{c ? a[0] : b[0], c ? a[1] : b[1]}; }
+HK_DEV int velocity_iterations_two(FSlot &s0, FSlot &s1, Dyn &B, int nc) {
+  if (nc == 0) return 0;
+  const bool two = nc == 2;
+  const int a0 = fs_bA(s0), b0 = fs_bB(s0);
+  const int a1 = two ? fs_bA(s1) : 15, b1 = two ? fs_bB(s1) : 15;  // 15: matches no body
+  const bool dA0 = a0 < 3, dA1 = a1 < 3;
+  const bool a1a0 = a1 == a0, a1b0 = a1 == b0, b1a0 = b1 == a0, b1b0 = b1 == b0;
+  v2 t;
+  float wA0, wB0, wA1, wB1;
+  get_vel_a(B, a0, t, wA0);
+  f2 vA0 = F2(t);
+  get_vel_b(B, b0, t, wB0);
+  f2 vB0 = F2(t);
+  get_vel_a(B, a1, t, wA1);
+  f2 vA1 = F2(t);
+  get_vel_b(B, b1, t, wB1);
+  f2 vB1 = F2(t);
+  uint32_t sn[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) sn[k] = 0u;
+  int it = 0;
+  bool active = true;
+  HK_MARK(vtwo_begin);
+  for (; it < kVelIters && active; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!dA0) {
+        vA0 = f2{0.0f, 0.0f};
+        wA0 = 0.0f;
+      }
+      fslot_solve_velocity_p(s0, vA0, wA0, vB0, wB0);
+      vA1 = sel2(a1a0, vA0, sel2(a1b0, vB0, vA1));
+      wA1 = a1a0 ? wA0 : (a1b0 ? wB0 : wA1);
+      vB1 = sel2(b1a0, vA0, sel2(b1b0, vB0, vB1));
+      wB1 = b1a0 ? wA0 : (b1b0 ? wB0 : wB1);
+      if (two) {
+        if (!dA1) {
+          vA1 = f2{0.0f, 0.0f};
+          wA1 = 0.0f;
+        }
+        fslot_solve_velocity_p(s1, vA1, wA1, vB1, wB1);
+        vA0 = sel2(a1a0, vA1, sel2(b1a0, vB1, vA0));
+        wA0 = a1a0 ? wA1 : (b1a0 ? wB1 : wA0);
+        vB0 = sel2(a1b0, vA1, sel2(b1b0, vB1, vB0));
+        wB0 = a1b0 ? wA1 : (b1b0 ? wB1 : wB0);
+      }
+    }
+    const uint32_t x[20] = {__float_as_uint(vB0[0]), __float_as_uint(vB0[1]), __float_as_uint(wB0),
+                            dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
+                            dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
+                            __float_as_uint(s0.ti[0]), __float_as_uint(s0.ti[1]),
+                            two ? __float_as_uint(vB1[0]) : 0u, two ? __float_as_uint(vB1[1]) : 0u,
+                            two ? __float_as_uint(wB1) : 0u, dA1 ? __float_as_uint(vA1[0]) : 0u,
+                            dA1 ? __float_as_uint(vA1[1]) : 0u, dA1 ? __float_as_uint(wA1) : 0u,
+                            two ? __float_as_uint(s1.ni[0]) : 0u, two ? __float_as_uint(s1.ni[1]) : 0u,
+                            two ? __float_as_uint(s1.ti[0]) : 0u, two ? __float_as_uint(s1.ti[1]) : 0u};
+    uint32_t diff = 0u;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+      diff |= x[k] ^ sn[k];
+      sn[k] = x[k];
+    }
+    if (it + 3 >= 7 && diff == 0u) active = false;
+  }
+  HK_MARK(vtwo_end);
+  if (dA0) set_vel_a(B, a0, V2(vA0), wA0);
+  set_vel_b(B, b0, V2(vB0), wB0);
+  if (two) {
+    if (dA1) set_vel_a(B, a1, V2(vA1), wA1);
+    set_vel_b(B, b1, V2(vB1), wB1);
+  }
+  return it;
+}
+
 // 180 velocity iterations over nc slots, with the exact periodic early exit
 template <typename SL>
 HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
-  if constexpr (SL::kRegister && SL::kOneFast) {
-    if constexpr (SL::kWaveGated) {
-      // island solves: the one-contact loop only when no active lane of the wave solves a larger island,
-      // so a wave never runs both loops one after the other (which would lengthen the slowest waves)
-      const bool multi = wave_any(nc > 1);
-      if (nc == 1 && !multi) return velocity_iterations_one(S.s[0], B);
-    } else {
+  if constexpr (SL::kRegister) {
+    // the one-contact loop only when no active lane of the wave solves a larger island, the two-contact
+    // loop (which also serves the wave's one-contact lanes) only when none solves more than two: a wave
+    // never runs two of these loops one after the other (which would lengthen the slowest waves)
+    if (!wave_any(nc > 1)) {
       if (nc == 1) return velocity_iterations_one(S.s[0], B);
+    } else if (!wave_any(nc > 2)) {
+      return velocity_iterations_two(S.s[0], S.s[1], B, nc);
     }
   }
   uint32_t sb[9];
