@@ -242,7 +242,18 @@ HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
 
 // one b2ContactSolver::SolveVelocityConstraints pass over one contact (tangent rows, then the normal row or the
 // 2-point block solver), on the two bodies' velocities held in locals; the 2-vector arithmetic is packed fp32
-// (f2) with Box2D's float operations in Box2D's order
+// relative velocity at a contact point, dv = vB + wB x rB - vA - wA x rA (Box2D's operation order)
+template <bool kSA>
+HK_DEV f2 rel_vel(f2 vA, float wA, f2 vB, float wB, f2 rA, f2 rB) {
+  if constexpr (kSA) return (vB + bc(wB) * perp(rB)) - bc(0.0f) * perp(rA);
+  else return ((vB + bc(wB) * perp(rB)) - vA) - bc(wA) * perp(rA);
+}
+
+// (f2) with Box2D's float operations in Box2D's order.
+// kSA: body A is static, so vA = wA = +0 at every solve (the callers reset them) and A's updates are dead.
+// The relative velocity then keeps only the operations that can change a bit: u - (+0) == u for every u,
+// but u - (+0)*perp(rA) can turn a -0 of u into +0, so that product stays (loop-invariant, hoisted).
+template <bool kSA = false>
 HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &wB) {
   const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
   const int vcount = fs_vcount(s);
@@ -251,7 +262,7 @@ HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &w
   for (int j = 0; j < 2; ++j) {
     if (j < vcount) {
       const f2 rA = f2{s.rAx[j], s.rAy[j]}, rB = f2{s.rBx[j], s.rBy[j]};
-      const f2 dv = ((vB + bc(wB) * perp(rB)) - vA) - bc(wA) * perp(rA);
+      const f2 dv = rel_vel<kSA>(vA, wA, vB, wB, rA, rB);
       float vt = pdot(dv, tangent) - 0.0f;
       float lambda = s.tm[j] * (-vt);
       float maxF = s.fr * s.ni[j];
@@ -259,31 +270,35 @@ HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &w
       lambda = newI - s.ti[j];
       s.ti[j] = newI;
       const f2 P = bc(lambda) * tangent;
-      vA = vA - bc(mA) * P;
-      wA -= iA * pcrs(rA, P);
+      if constexpr (!kSA) {
+        vA = vA - bc(mA) * P;
+        wA -= iA * pcrs(rA, P);
+      }
       vB = vB + bc(mB) * P;
       wB += iB * pcrs(rB, P);
     }
   }
   if (vcount == 1) {
     const f2 rA = f2{s.rAx[0], s.rAy[0]}, rB = f2{s.rBx[0], s.rBy[0]};
-    const f2 dv = ((vB + bc(wB) * perp(rB)) - vA) - bc(wA) * perp(rA);
+    const f2 dv = rel_vel<kSA>(vA, wA, vB, wB, rA, rB);
     float vn = pdot(dv, normal);
     float lambda = -s.nm[0] * (vn - s.bias[0]);
     float newI = fmax2(s.ni[0] + lambda, 0.0f);
     lambda = newI - s.ni[0];
     s.ni[0] = newI;
     const f2 P = bc(lambda) * normal;
-    vA = vA - bc(mA) * P;
-    wA -= iA * pcrs(rA, P);
+    if constexpr (!kSA) {
+      vA = vA - bc(mA) * P;
+      wA -= iA * pcrs(rA, P);
+    }
     vB = vB + bc(mB) * P;
     wB += iB * pcrs(rB, P);
   } else {
     const f2 r1A = f2{s.rAx[0], s.rAy[0]}, r1B = f2{s.rBx[0], s.rBy[0]};
     const f2 r2A = f2{s.rAx[1], s.rAy[1]}, r2B = f2{s.rBx[1], s.rBy[1]};
     v2 a = V(s.ni[0], s.ni[1]);
-    const f2 dv1 = ((vB + bc(wB) * perp(r1B)) - vA) - bc(wA) * perp(r1A);
-    const f2 dv2 = ((vB + bc(wB) * perp(r2B)) - vA) - bc(wA) * perp(r2A);
+    const f2 dv1 = rel_vel<kSA>(vA, wA, vB, wB, r1A, r1B);
+    const f2 dv2 = rel_vel<kSA>(vA, wA, vB, wB, r2A, r2B);
     float vn1 = pdot(dv1, normal), vn2 = pdot(dv2, normal);
     v2 b;
     b.x = vn1 - s.bias[0];
@@ -314,8 +329,10 @@ HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &w
     if (ok) {
       const v2 d = vsub(x, a);
       const f2 P1 = bc(d.x) * normal, P2 = bc(d.y) * normal;
-      vA = vA - bc(mA) * (P1 + P2);
-      wA -= iA * (pcrs(r1A, P1) + pcrs(r2A, P2));
+      if constexpr (!kSA) {
+        vA = vA - bc(mA) * (P1 + P2);
+        wA -= iA * (pcrs(r1A, P1) + pcrs(r2A, P2));
+      }
       vB = vB + bc(mB) * (P1 + P2);
       wB += iB * (pcrs(r1B, P1) + pcrs(r2B, P2));
       s.ni[0] = x.x;
@@ -470,9 +487,10 @@ template <> struct SlotCap<HbmSlots> { static constexpr int value = kBigC; };
 // velocities stay in locals for the whole loop instead of round-tripping through the body file's selects
 // every iteration.  A static body's velocity is re-read as +0 at every iteration, exactly what get_vel
 // returns in the general loop; the snapshot compares the same values the general loop compares.
-HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
+template <bool kSA>
+HK_DEV int velocity_iterations_one_t(FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s);
-  const bool dynA = bA < 3;
+  const bool dynA = !kSA && bA < 3;
   v2 vA2, vB2;
   float wA, wB;
   get_vel_a(B, bA, vA2, wA);
@@ -491,7 +509,7 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
         vA = f2{0.0f, 0.0f};
         wA = 0.0f;
       }
-      fslot_solve_velocity_p(s, vA, wA, vB, wB);
+      fslot_solve_velocity_p<kSA>(s, vA, wA, vB, wB);
     }
     const uint32_t x[10] = {__float_as_uint(vB[0]), __float_as_uint(vB[1]), __float_as_uint(wB),
                             dynA ? __float_as_uint(vA[0]) : 0u, dynA ? __float_as_uint(vA[1]) : 0u,
@@ -509,6 +527,12 @@ HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
   if (dynA) set_vel_a(B, bA, V2(vA), wA);
   set_vel_b(B, bB, V2(vB), wB);
   return it;
+}
+// waves whose one-contact solves all have a static body A (every TOI solve, wall contacts) take the
+// static-A row
+HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
+  if (!wave_any(fs_bA(s) < 3)) return velocity_iterations_one_t<true>(s, B);
+  return velocity_iterations_one_t<false>(s, B);
 }
 
 // Two-contact solve (waves whose islands all have at most two contacts; a one-contact lane runs it with
