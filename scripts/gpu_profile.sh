@@ -24,4 +24,5 @@ rm -rf gpurun_out/prof
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
   python3 bench.py --no-cpu-baseline --streams 0 > $O/prof_bench.log 2>&1
 find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+find gpurun_out/prof -name "*kernel_trace.csv" -exec cp {} $O/kernel_trace.csv \;
 head -3 $O/kernel_stats.csv
