@@ -37,7 +37,9 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rollout", type=int, default=50,
                     help="also time hk_rollout with this many steps per launch (0 = skip); reported under 'rollout'")
-    ap.add_argument("--cpu-arenas", type=int, default=32768, help="CPU baseline sample: arenas x 250 steps")
+    ap.add_argument("--cpu-arenas", type=int, default=32768, help="CPU baseline sample: arenas per step")
+    ap.add_argument("--cpu-steps", type=int, default=1000,
+                    help="CPU baseline sample: steps (32768 x 1000 is ~13 s on 16 host cores)")
     ap.add_argument("--streams", type=int, default=2,
                     help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
                          "reported under 'streams'")
@@ -56,14 +58,13 @@ def _traffic_from_profiles(n_arenas, policy):
         return None
 
 
-def cpu_baseline(policy, n_arenas):
+def cpu_baseline(policy, n_arenas, steps):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # the checker, timed as the CPU baseline (kind "port")
 
     O.build()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
-    steps = 250
     total, sec = O.bench_random(n_arenas, steps, threads, 0, policy)
     return {"value": total / sec, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_arenas} arenas x {steps} steps ({'strong-vs-strong BasicOpponent' if policy == 'basic' else 'random actions'}, "
@@ -265,7 +266,7 @@ def main():
         if streams is not None:
             line["streams"] = streams
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas)
+            line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_steps)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:
