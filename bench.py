@@ -11,8 +11,14 @@ Multi-GPU (weak scaling, no data-path collective: arenas are independent, SURVEY
 GPU, launched by torch.distributed.run; rank r owns global arenas [r*N, (r+1)*N).  The timed region is
 bracketed by barrier + synchronize on every rank and the max over ranks is reported.
 
-Output: ONE JSON line on rank 0 with `roofline` (step kernel: algorithmic bytes / measured average
-kernel duration vs 8 TB/s HBM) and `cpu_baseline` (the C oracle on host cores, rank 0 at N=1 only).
+Steady state: before the warmup every arena is pre-rolled --preroll steps (default 1000, hk_rollout launches
+with no outputs, independent of --warmup), so the timed steps see desynchronised episodes at their steady
+contact / TOI load; the timed region must contain finished episodes (asserted).
+
+Output: ONE JSON line on rank 0 with `roofline` (step kernel, VALU-bound: active-lane VALU operations per
+launch from the committed rocprofv3 SQ counters / measured average kernel duration vs the fp32 VALU lane
+rate; `roofline.hbm`: algorithmic bytes / the same duration vs 8 TB/s) and `cpu_baseline` (the C oracle's
+batched context on the same workload on host cores, plus the C1 single-env number; rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -24,6 +30,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# fp32 VALU lane-operation peak: 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: 157.3 TFLOPS
+# counts an FMA as 2).  One wave per SIMD (this kernel's occupancy) issues a VALU op every 4 cycles, not 2.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
 def _args():
@@ -31,44 +40,93 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--preroll", type=int, default=1000,
+                    help="steps every arena is advanced (hk_rollout, no outputs) before the warmup, so the timed "
+                         "steps run at the steady episode mix whatever --warmup is")
     ap.add_argument("--arenas", type=int, default=65536, help="arenas per GPU")
     ap.add_argument("--policy", choices=["basic", "random"], default="basic")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rollout", type=int, default=50,
                     help="also time hk_rollout with this many steps per launch (0 = skip); reported under 'rollout'")
-    ap.add_argument("--cpu-arenas", type=int, default=32768, help="CPU baseline sample: arenas per step")
-    ap.add_argument("--cpu-steps", type=int, default=1000,
-                    help="CPU baseline sample: steps (32768 x 1000 is ~13 s on 16 host cores)")
+    ap.add_argument("--cpu-arenas", type=int, default=65536, help="CPU baseline sample: arenas (C3 size)")
+    ap.add_argument("--cpu-preroll", type=int, default=260, help="CPU baseline: untimed steps first (> 251)")
+    ap.add_argument("--cpu-steps", type=int, default=150,
+                    help="CPU baseline sample: timed steps (65536 x (260 + 150) is ~15 s on 16 host cores)")
     ap.add_argument("--streams", type=int, default=2,
                     help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
                          "reported under 'streams'")
     return ap.parse_args()
 
 
-def _traffic_from_profiles(n_arenas, policy):
-    """HBM bytes per step-kernel launch from the committed rocprofv3 PMC summary (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def _profile(name, key):
+    """profiles/<name>.json [key] (committed rocprofv3 summaries, scripts/pmc_reduce.py / sq_reduce.py), or None."""
     try:
-        with open(path) as f:
-            d = json.load(f)
-        key = f"{policy}_{n_arenas}"
-        return d[key]["hbm_bytes_per_launch"] if key in d else None
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            return json.load(f).get(key)
     except Exception:  # noqa: BLE001
         return None
 
 
-def cpu_baseline(policy, n_arenas, steps):
+def host_cores():
+    """CPU cores this process may run on (the box's CPU share: its affinity mask, capped by OMP_NUM_THREADS)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, omp) if omp > 0 else n)
+
+
+def cpu_baseline(policy, n_arenas, preroll, steps, seed):
+    """The oracle's batched context (the C restatement of HockeyEnv.step, oracle/hk_oracle.c) on the same
+    workload as the GPU line -- same policies, Philox streams, auto-reset -- on all host cores this process
+    may use; plus BASELINE C1 (one env, one thread)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
     import oracle as O  # the checker, timed as the CPU baseline (kind "port")
+    from hockey_amd.placement import np_random, placement
 
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    total, sec = O.bench_random(n_arenas, steps, threads, 0, policy)
-    return {"value": total / sec, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n_arenas} arenas x {steps} steps ({'strong-vs-strong BasicOpponent' if policy == 'basic' else 'random actions'}, "
-                      f"auto-reset) on the C restatement of HockeyEnv.step (oracle/hk_oracle.c), {sec:.1f} s"}
+    cores = host_cores()
+    pol = ("strong", "strong") if policy == "basic" else ("random", "random")
+    ov = O.OracleVec(n_arenas, policies=pol, auto_reset=True, seed=seed)
+    pre = ov.time_steps(preroll, cores)
+    sec = ov.time_steps(steps, cores)
+    ep = int(ov.counters()[1])
+    ov.close()
+    # C1 (SURVEY §8d): BasicOpponent(weak) vs U(-1,1) from default_rng(0), np.random.seed(0) phase stream,
+    # reset(seed=episode) on done, 10 000 steps, 1 thread
+    c1_steps = 10_000
+    p2 = np.random.default_rng(0).uniform(-1, 1, (c1_steps, 4)).astype(np.float32)
+    legacy = np.random.RandomState(0)
+    phase0 = legacy.uniform(0, np.pi)
+    inc = legacy.uniform(0, 0.2, c1_steps)
+    params, one = [], True
+    for e in range(400):
+        one = not one
+        rng, _ = np_random(e)
+        params.append(placement(0, one, rng)[0])
+    _, _, c1_eps, c1_sec = O.run_c1(p2, inc, phase0, np.stack(params), record=False)
+    return {"value": n_arenas * steps / sec, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{n_arenas} arenas x {steps} timed steps after {preroll} untimed ({pre:.1f} s), "
+                      f"{'strong-vs-strong BasicOpponent' if policy == 'basic' else 'random actions'} with the GPU "
+                      f"line's Philox streams and auto-reset ({ep} episodes finished), batched C restatement of "
+                      f"HockeyEnv.step (oracle/hk_oracle.c hkov_*), OpenMP over arenas, {sec:.1f} s",
+            "single_env": {"value": c1_steps / c1_sec, "unit": "env-steps/s", "cores": 1,
+                           "sample": f"BASELINE C1: 1 env, BasicOpponent(weak) vs U(-1,1), reset(seed=episode) on "
+                                     f"done, {c1_steps} steps ({c1_eps} episodes), 1 thread, {c1_sec:.3f} s"}}
+
+
+def preroll(env, steps, N):
+    """Advance every arena `steps` steps with no outputs (hk_rollout launches of at most 250 steps)."""
+    io = N.StepIO()
+    left = steps
+    while left > 0:
+        k = min(250, left)
+        env.rollout_raw(k, io)
+        left -= k
 
 
 def reduce_over_ranks(elapsed, counters, dist, device):
@@ -135,6 +193,7 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
         e = VecHockeyEnv(m, device=dev, policies=pol, auto_reset=True, seed=args.seed,
                          arena_offset=shard_offset(rank, n) + k * m)
         e.reset()
+        preroll(e, args.preroll, N)
         io = N.StepIO()
         io.obs, io.reward, io.done, io.info = (e.obs_buf.data_ptr(), e.reward_buf.data_ptr(),
                                                e.done_buf.data_ptr(), e.info_buf.data_ptr())
@@ -197,6 +256,7 @@ def main():
     io.done = env.done_buf.data_ptr()
     io.info = env.info_buf.data_ptr()
 
+    preroll(env, args.preroll, N)
     for _ in range(args.warmup):
         env.step_raw(io)
     torch.cuda.synchronize()
@@ -231,11 +291,17 @@ def main():
     total_steps = n * world * args.steps
     assert int(cnt[N.CNT_STEPS]) == total_steps, (cnt, total_steps)
     assert int(cnt[N.CNT_OVERFLOW]) == 0, cnt
+    assert int(cnt[N.CNT_EPISODES]) > 0, "timed region holds no finished episode: not at steady state"
     value = total_steps / elapsed
 
     if rank == 0:
         alg_bytes, impl_bytes = env.bytes_per_step()
-        achieved = alg_bytes * n / (kern_ms * 1e-3) / 1e9
+        hbm_gbs = alg_bytes * n / (kern_ms * 1e-3) / 1e9
+        key = f"{args.policy}_{n}"
+        pmc = _profile("pmc_summary.json", key) or {}
+        sq = _profile("sq_summary.json", key) or {}
+        lane_ops = sq.get("valu_lane_ops_per_launch")
+        valu_tops = lane_ops / (kern_ms * 1e-3) / 1e12 if lane_ops else None
         line = {
             "metric": "env-steps/sec at 65536 arenas per MI355X (BASELINE.json metric)",
             "value": value,
@@ -253,11 +319,18 @@ def main():
                                    f"{'strong-vs-strong BasicOpponent on-GPU' if args.policy == 'basic' else 'random-vs-random'}"
                                    f", auto-reset", "arenas_per_gpu": n, "policy": args.policy,
                        "parallelism": f"arena-sharded x{world} (no collectives)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": _traffic_from_profiles(n, args.policy),
+            "roofline": {"bound": "valu", "achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+                         "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
+                         "traffic": pmc.get("hbm_bytes_per_launch"),
                          "kernel": "hk::step_kernel", "kernel_avg_ms": kern_ms,
-                         "algorithmic_bytes_per_env_step": alg_bytes},
+                         "valu_lane_ops_per_launch": lane_ops,
+                         "valu_issue_util": sq.get("valu_issue_util"), "valu_lane_util": sq.get("valu_lane_util"),
+                         "counters_from": sq.get("source"),
+                         "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": hbm_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": alg_bytes,
+                                 "traffic_bytes_per_launch": pmc.get("hbm_bytes_per_launch"),
+                                 "traffic_from": pmc.get("source")}},
+            "preroll": args.preroll,
             "episodes": int(cnt[N.CNT_EPISODES]),
             "toi_events": int(cnt[N.CNT_TOI]),
         }
@@ -266,7 +339,8 @@ def main():
         if streams is not None:
             line["streams"] = streams
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_steps)
+            line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_preroll, args.cpu_steps,
+                                                args.seed)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:

@@ -575,9 +575,6 @@ HK_DEV void collide(Arena &w) {
       const int p = __ffs(near) - 1;
       near &= near - 1u;
       pair_update_near(w, p);
-#ifdef HK_X_DUP_NEAR
-      { int p2 = p; asm volatile("" : "+v"(p2)); pair_update_near(w, p2); }
-#endif
     }
     return;
   }
@@ -783,9 +780,6 @@ HK_DEV void toi_drain(Arena &w, uint32_t &pending, uint32_t &below) {
     const int p = __ffs(pending) - 1;
     pending &= pending - 1u;
     float alpha = toi_pair(w, p);
-#ifdef HK_X_DUP_TOI
-    { int p2 = p; asm volatile("" : "+v"(p2)); const float a2 = toi_pair(w, p2); asm volatile("" :: "v"(a2)); }
-#endif
     LDS(w, kLdsToi + p) = alpha;
     below = alpha < 1.0f ? (below | (1u << p)) : (below & ~(1u << p));
   }

@@ -59,7 +59,7 @@ extern "C" {
 
 const char *hk_last_error(void) { return g_err.c_str(); }
 
-const char *hk_version(void) { return "hockey-mi355x 0.1 (gfx950, lane-per-arena step kernel)"; }
+const char *hk_version(void) { return "hockey-mi355x 0.2 (gfx950, lane-per-arena step kernel)"; }
 
 int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   if (!out) return fail(HK_E_INVALID, "hk_create: out is NULL%s", "");
@@ -69,6 +69,7 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   if (cfg->mode < 0 || cfg->mode > 2) return fail(HK_E_INVALID, "hk_create: bad mode%s");
   if (!check_policy(cfg->policy[0]) || !check_policy(cfg->policy[1]))
     return fail(HK_E_INVALID, "hk_create: bad policy%s");
+  if (cfg->diag_flags & ~HK_DIAG_LARGE_ISLANDS) return fail(HK_E_INVALID, "hk_create: unknown diag_flags%s");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0) return fail(HK_E_DEVICE, "hk_create: no HIP device available%s");
@@ -88,8 +89,7 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   c->cfg.policy[1] = cfg->policy[1];
   c->cfg.seed = cfg->seed;
   c->cfg.arena_offset = cfg->arena_offset;
-  c->cfg.ablate = 0;
-  if (const char *ab = std::getenv("HK_ABLATE")) c->cfg.ablate = std::atoi(ab);  // timing experiments only
+  c->cfg.diag = cfg->diag_flags;
   c->s.n = n;
   const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NIF * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
   const size_t nw = (size_t)hk::workspace_words_per_arena() * n;
@@ -168,6 +168,7 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
   s.info2 = io->info2;
   s.actions_out = io->actions_out;
   s.debug = io->debug;
+  s.final_obs = io->final_obs;
   s.flags = io->flags;
   DeviceGuard g(c->device);
   hipError_t e = hk::launch_step(c->s, c->cfg, s, nsteps, (hipStream_t)stream);

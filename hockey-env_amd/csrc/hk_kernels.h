@@ -34,7 +34,7 @@ struct KCfg {
   int policy[2];
   uint64_t seed;
   int64_t arena_offset;
-  int ablate;  // diagnostics only (HK_ABLATE env): bit0 forces the generic large-island solver; 0 in product
+  int diag;  // hk_config.diag_flags (HK_DIAG_*): bit0 routes every solve through the HBM slot file; 0 in product
 };
 
 struct StepIO {
@@ -42,7 +42,7 @@ struct StepIO {
   const double *opp_inc;
   float *obs, *obs2, *reward, *reward2;
   uint8_t *done;
-  float *info, *info2, *actions_out, *debug;
+  float *info, *info2, *actions_out, *debug, *final_obs;
   int flags;
 };
 

@@ -242,29 +242,18 @@ HK_DEV void reset_lane(const DevState &s, const KCfg &cfg, int64_t a, const floa
   I(s, I_EPISODE, a) = I(s, I_EPISODE, a) + 1;
 }
 
-// One HockeyEnv.step of arena a (auto-reset, policy actions, pre-solve laws, world.Step, outputs).
+// One HockeyEnv.step of arena a (policy actions, pre-solve laws, world.Step, outputs, then auto-reset).
 struct LaneOut { int done_edge, win1, win2, ntoi, ovf, nbig; };
 
 HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int64_t a, float *lds, int lane,
                       PhaseT &T, LaneOut &out) {
   Arena w;
   load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, lds, lane);
-  w.force_big = cfg.ablate & 1;
+  w.force_big = cfg.diag & 1;
 #ifdef HK_TRACE
   w.trace = io.debug ? io.debug + a * kTraceStride : nullptr;
 #endif
   const uint32_t stepc = (uint32_t)I(s, I_STEP, a);
-  if (cfg.auto_reset && w.done) {
-    int one = I(s, I_ONE, a);
-    if (cfg.mode == 0) one = !one;
-    const uint32_t ep = (uint32_t)I(s, I_EPISODE, a);
-    float p6[6];
-    int mt;
-    device_placement(cfg.seed, cfg.arena_offset + a, ep, cfg.mode, one, p6, mt);
-    reset_arena(w, p6, mt);
-    I(s, I_ONE, a) = one;
-    I(s, I_EPISODE, a) = (int)(ep + 1);
-  }
   // ---- actions: external / Philox random / fused BasicOpponent ----
   float a8[8];
   for (int p = 0; p < 2; ++p) {
@@ -320,20 +309,15 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     for (int b = 0; b < 3; ++b) { w.d.fx[b] = 0.0f; w.d.fy[b] = 0.0f; w.d.tq[b] = 0.0f; }
   }
   float o[18];
-  if (io.obs) {
-    observe(w, o);
-    for (int k = 0; k < 18; ++k) io.obs[a * 18 + k] = o[k];
-  }
+  observe(w, o);
+  if (io.final_obs)
+    for (int k = 0; k < 18; ++k) io.final_obs[a * 18 + k] = o[k];
   if (w.time >= w.max_t) w.done = 1;
   double info[4];
   info_side<0>(w, info);
   if (io.info) write_info(io.info, a, info);
   if (io.reward) io.reward[a] = (float)(compute_reward(w) + info[1]);
-  if (io.obs2 || io.info2 || io.reward2) {
-    if (io.obs2) {
-      observe_two(w, o);
-      for (int k = 0; k < 18; ++k) io.obs2[a * 18 + k] = o[k];
-    }
+  if (io.info2 || io.reward2) {
     double info2[4];
     info_side<1>(w, info2);
     if (io.info2) write_info(io.info2, a, info2);
@@ -341,12 +325,31 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   }
   if (io.done) io.done[a] = (uint8_t)w.done;
   w.time += 1;
+  const int done_edge = !was_done && w.done, winner = w.winner;
+  if (cfg.auto_reset && w.done) {  // the next episode starts now; obs / obs2 describe its first state
+    int one = I(s, I_ONE, a);
+    if (cfg.mode == 0) one = !one;
+    const uint32_t ep = (uint32_t)I(s, I_EPISODE, a);
+    float p6[6];
+    int mt;
+    device_placement(cfg.seed, cfg.arena_offset + a, ep, cfg.mode, one, p6, mt);
+    reset_arena(w, p6, mt);
+    I(s, I_ONE, a) = one;
+    I(s, I_EPISODE, a) = (int)(ep + 1);
+    observe(w, o);
+  }
+  if (io.obs)
+    for (int k = 0; k < 18; ++k) io.obs[a * 18 + k] = o[k];
+  if (io.obs2) {
+    observe_two(w, o);
+    for (int k = 0; k < 18; ++k) io.obs2[a * 18 + k] = o[k];
+  }
   store_arena(w, s, a);
   I(s, I_STEP, a) = (int)(stepc + 1);
   HK_TIC(T, 12);  // diagnostics: outputs and state store
-  out.done_edge = (!was_done && w.done);
-  out.win1 = out.done_edge && w.winner == 1;
-  out.win2 = out.done_edge && w.winner == -1;
+  out.done_edge = done_edge;
+  out.win1 = done_edge && winner == 1;
+  out.win2 = done_edge && winner == -1;
   out.ntoi = w.n_toi;
   out.ovf = w.overflow;
   out.nbig = w.n_big;

@@ -53,7 +53,7 @@ struct HostCtx {
 
 extern "C" {
 
-// cfg = {keep_mode, mode, auto_reset, vel_ref, policy0, policy1}; seed; arena_offset
+// cfg = {keep_mode, mode, auto_reset, vel_ref, policy0, policy1, diag_flags}; seed; arena_offset
 void *hkh_create(int64_t n, const int *cfg6, uint64_t seed, int64_t arena_offset) {
   HostCtx *c = new HostCtx();
   c->n = n;
@@ -80,7 +80,7 @@ void *hkh_create(int64_t n, const int *cfg6, uint64_t seed, int64_t arena_offset
   c->cfg.policy[1] = cfg6[5];
   c->cfg.seed = seed;
   c->cfg.arena_offset = arena_offset;
-  if (const char *ab = std::getenv("HK_ABLATE")) c->cfg.ablate = std::atoi(ab);
+  c->cfg.diag = cfg6[6];
   for (int64_t a = 0; a < n; ++a) init_lane(c->s, c->cfg, a);
   return c;
 }

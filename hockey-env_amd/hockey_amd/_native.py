@@ -16,6 +16,7 @@ OBS_DIM, ACT_DIM, INFO_DIM, STATE_DIM, AUX_DIM, PARAM_DIM, DEBUG_DIM, NUM_COUNTE
 
 POLICY_EXTERNAL, POLICY_RANDOM, POLICY_BASIC_WEAK, POLICY_BASIC_STRONG = 0, 1, 2, 3
 STEP_SKIP_PHYSICS = 1
+DIAG_LARGE_ISLANDS = 1
 CNT_STEPS, CNT_EPISODES, CNT_GOALS_P1, CNT_GOALS_P2, CNT_TOI, CNT_OVERFLOW = range(6)
 
 
@@ -26,14 +27,15 @@ class HockeyNativeError(RuntimeError):
 class Config(ctypes.Structure):
     _fields_ = [("keep_mode", ctypes.c_int32), ("mode", ctypes.c_int32), ("auto_reset", ctypes.c_int32),
                 ("vel_ref_semantics", ctypes.c_int32), ("policy", ctypes.c_int32 * 2), ("seed", ctypes.c_uint64),
-                ("arena_offset", ctypes.c_int64)]
+                ("arena_offset", ctypes.c_int64), ("diag_flags", ctypes.c_int32)]
 
 
 class StepIO(ctypes.Structure):
     _fields_ = [("actions", ctypes.c_void_p), ("opp_inc", ctypes.c_void_p), ("obs", ctypes.c_void_p),
                 ("obs2", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("reward2", ctypes.c_void_p),
                 ("done", ctypes.c_void_p), ("info", ctypes.c_void_p), ("info2", ctypes.c_void_p),
-                ("actions_out", ctypes.c_void_p), ("debug", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+                ("actions_out", ctypes.c_void_p), ("debug", ctypes.c_void_p), ("final_obs", ctypes.c_void_p),
+                ("flags", ctypes.c_int32)]
 
 
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",

@@ -36,7 +36,7 @@ def _policy_id(p):
 
 
 class StepResult:
-    __slots__ = ("obs", "reward", "done", "info", "obs2", "reward2", "info2", "actions")
+    __slots__ = ("obs", "reward", "done", "info", "obs2", "reward2", "info2", "actions", "final_obs")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -47,7 +47,7 @@ class VecHockeyEnv:
     """Batched hockey arenas on one MI355X (one context per device and stream)."""
 
     def __init__(self, n_arenas, keep_mode=True, mode=Mode.NORMAL, device=None, policies=("external", "external"),
-                 auto_reset=False, seed=0, vel_ref_semantics=False, arena_offset=0):
+                 auto_reset=False, seed=0, vel_ref_semantics=False, arena_offset=0, diag_flags=0):
         if not torch.cuda.is_available():
             raise N.HockeyNativeError("VecHockeyEnv needs a ROCm GPU (gfx950); the hot path has no CPU fallback")
         self.L = N.lib()
@@ -65,6 +65,7 @@ class VecHockeyEnv:
         cfg.policy[1] = _policy_id(policies[1])
         cfg.seed = int(seed) & ((1 << 64) - 1)
         cfg.arena_offset = int(arena_offset)
+        cfg.diag_flags = int(diag_flags)
         self.arena_offset = int(arena_offset)
         self.policies = [cfg.policy[0], cfg.policy[1]]
         ctx = ctypes.c_void_p()
@@ -85,6 +86,7 @@ class VecHockeyEnv:
         self.info_buf = torch.zeros((n, N.INFO_DIM), dtype=torch.float32, device=d)
         self.info2_buf = torch.zeros((n, N.INFO_DIM), dtype=torch.float32, device=d)
         self.actions_buf = torch.zeros((n, N.ACT_DIM), dtype=torch.float32, device=d)
+        self.final_obs_buf = torch.zeros((n, N.OBS_DIM), dtype=torch.float32, device=d)
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -144,9 +146,13 @@ class VecHockeyEnv:
 
     # ------------------------------------------------------------------ step
     def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=None, skip_physics=False,
-             record_actions=False):
+             record_actions=False, final_obs=False):
         """HockeyEnv.step for every arena.  actions: [N,8] float (clipped in-kernel), may be None when no
-        player is external.  Returns a StepResult of device tensors (views of persistent buffers)."""
+        player is external.  Returns a StepResult of device tensors (views of persistent buffers).
+
+        With auto_reset, an arena that is done after this step is reset at its end: done / reward / info are
+        the terminal step's, obs / obs2 the new episode's first state, and ``final_obs`` (when requested) the
+        terminal observation (== obs for arenas that did not reset)."""
         a = None
         if actions is not None:
             a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
@@ -171,19 +177,22 @@ class VecHockeyEnv:
             io.actions_out = self.actions_buf.data_ptr()
         if debug is not None:
             io.debug = debug.data_ptr()
+        if final_obs:
+            io.final_obs = self.final_obs_buf.data_ptr()
         io.flags = N.STEP_SKIP_PHYSICS if skip_physics else 0
         N.check(self.L.hk_step(self._ctx, ctypes.byref(io), self._stream()), "hk_step")
         return StepResult(obs=self.obs_buf, reward=self.reward_buf, done=self.done_buf, info=self.info_buf,
                           obs2=self.obs2_buf if with_agent_two else None,
                           reward2=self.reward2_buf if with_agent_two else None,
                           info2=self.info2_buf if with_agent_two else None,
-                          actions=self.actions_buf if record_actions else None)
+                          actions=self.actions_buf if record_actions else None,
+                          final_obs=self.final_obs_buf if final_obs else None)
 
     def step_raw(self, io):
         """Launch one step with a prepared StepIO (no Python-side allocation; for benchmarks)."""
         N.check(self.L.hk_step(self._ctx, ctypes.byref(io), self._stream()), "hk_step")
 
-    def rollout(self, n_steps, actions=None, with_agent_two=False, record_actions=False):
+    def rollout(self, n_steps, actions=None, with_agent_two=False, record_actions=False, final_obs=False):
         """``n_steps`` consecutive steps in one launch (hk_rollout).  Returns a StepResult whose tensors carry a
         leading [n_steps] dimension.  ``actions`` ([n_steps, N, 8]) is needed only for external players."""
         k, n = int(n_steps), self.n
@@ -210,9 +219,13 @@ class VecHockeyEnv:
         if record_actions:
             acts = torch.empty((k, n, N.ACT_DIM), dtype=torch.float32, device=d)
             io.actions_out = acts.data_ptr()
+        fobs = None
+        if final_obs:
+            fobs = torch.empty_like(obs)
+            io.final_obs = fobs.data_ptr()
         N.check(self.L.hk_rollout(self._ctx, k, ctypes.byref(io), self._stream()), "hk_rollout")
         return StepResult(obs=obs, reward=rew, done=done, info=info, obs2=obs2, reward2=rew2, info2=info2,
-                          actions=acts)
+                          actions=acts, final_obs=fobs)
 
     def rollout_raw(self, n_steps, io):
         """hk_rollout with a prepared StepIO whose arrays have a leading [n_steps] dimension."""

@@ -70,14 +70,23 @@ enum {
 typedef struct hk_config {
   int32_t keep_mode;         /* HockeyEnv(keep_mode=True)  hockey_env.py:91 */
   int32_t mode;              /* 0 NORMAL, 1 TRAIN_SHOOTING, 2 TRAIN_DEFENSE (Mode, :78-81) */
-  int32_t auto_reset;        /* 0 = reference semantics (sticky done, :685-695); 1 = a done arena is
-                                reset (device placement) at the start of its next step */
+  int32_t auto_reset;        /* 0 = reference semantics (sticky done, :685-695); 1 = an arena that is done
+                                after a step is reset (device placement) at the end of that same step:
+                                done / reward / info describe the terminal step, obs / obs2 the new
+                                episode's first state, io.final_obs the terminal observation */
   int32_t vel_ref_semantics; /* 0 = pybox2d copy semantics (default) */
   int32_t policy[2];         /* HK_POLICY_* for player 1 and player 2 */
   uint64_t seed;             /* Philox key for device randomness */
   int64_t arena_offset;      /* global id of local arena 0: RNG streams are keyed by global arena id, so a
                                 shard of a multi-GPU run reproduces the same arenas bit for bit */
+  int32_t diag_flags;        /* HK_DIAG_* (0 in production): test-only routing of bit-identical slow paths */
 } hk_config;
+
+/* hk_config.diag_flags */
+enum {
+  HK_DIAG_LARGE_ISLANDS = 1 /* solve every island / TOI mini-island on the HBM slot file (the path islands
+                               larger than the register slots take, ~1e-5 of arena-steps); same results */
+};
 
 typedef struct hk_step_io {
   const float *actions;   /* [N,8] f32 joint action (external players), may be NULL if none external */
@@ -91,6 +100,8 @@ typedef struct hk_step_io {
   float *info2;           /* [N,4]  f32 agent-2 info (or NULL) */
   float *actions_out;     /* [N,8]  f32 joint action actually applied (or NULL) */
   float *debug;           /* [N,13] f32 pre-solve forces / torques / dampings (or NULL) */
+  float *final_obs;       /* [N,18] f32 observation after the step's physics (or NULL): the terminal
+                             observation of arenas that auto-reset in this step, == obs for the others */
   int32_t flags;          /* HK_STEP_* */
 } hk_step_io;
 

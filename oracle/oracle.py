@@ -48,9 +48,26 @@ def lib():
         L.hko_basic_opponent.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.c_double, _f64p, _f64p]
         L.hko_stats.argtypes = [ctypes.c_void_p, _i32p]
-        L.hko_bench_random.restype = ctypes.c_int64
-        L.hko_bench_random.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
-                                       ctypes.POINTER(ctypes.c_double)]
+        L.hko_set_vel_ref.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+        L.hko_philox.argtypes = [ctypes.c_uint64, u32p, u32p]
+        vp = ctypes.c_void_p
+        L.hkov_create.restype = vp
+        L.hkov_create.argtypes = [ctypes.c_int64, _i32p, ctypes.c_uint64, ctypes.c_int64]
+        L.hkov_destroy.argtypes = [vp]
+        L.hkov_reset.argtypes = [vp, vp, vp, vp, vp]
+        L.hkov_set_policy.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.hkov_step.argtypes = [vp] * 12
+        L.hkov_get_state.argtypes = [vp, vp, vp]
+        L.hkov_set_state.argtypes = [vp, vp, vp, vp]
+        L.hkov_observe.argtypes = [vp, vp, vp]
+        L.hkov_phase.argtypes = [vp, vp, vp]
+        L.hkov_counters.argtypes = [vp, vp]
+        L.hkov_time_steps.restype = ctypes.c_double
+        L.hkov_time_steps.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.hko_run_c1.restype = ctypes.c_int
+        L.hko_run_c1.argtypes = [ctypes.c_int, _f32p, _f64p, ctypes.c_double, _f32p, ctypes.c_int, vp, vp,
+                                 ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -58,11 +75,13 @@ def lib():
 class OracleWorld:
     """One arena of the CPU restatement (HockeyEnv + Box2D-2.3 step)."""
 
-    def __init__(self, keep_mode=True, mode=0):
+    def __init__(self, keep_mode=True, mode=0, vel_ref=False):
         self._L = lib()
         self.keep_mode = bool(keep_mode)
         self.mode = int(mode)
         self._w = self._L.hko_create(int(keep_mode), int(mode))
+        if vel_ref:
+            self._L.hko_set_vel_ref(self._w, 1)
 
     def __del__(self):
         try:
@@ -129,8 +148,115 @@ def geometry():
     return out[:n]
 
 
-def bench_random(n_arenas, steps, threads=0, seed=0, policy="random"):
+def philox(key, ctr):
+    """Philox4x32-10 block: key (uint64), counter (4 x uint32) -> 4 x uint32."""
+    out = np.zeros(4, np.uint32)
+    lib().hko_philox(int(key), np.ascontiguousarray(ctr, np.uint32), out)
+    return out
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+POLICY = {"external": 0, "random": 1, "weak": 2, "strong": 3}
+
+
+class OracleVec:
+    """N arenas of the CPU restatement behind the hk_create / hk_reset / hk_step contract (include/hockey.h):
+    fused policies, Philox randomness keyed by global arena id, auto-reset.  numpy in / out, [N, k] arrays."""
+
+    def __init__(self, n, keep_mode=True, mode=0, auto_reset=False, vel_ref=False, policies=("external", "external"),
+                 seed=0, arena_offset=0):
+        self._L = lib()
+        self.n = int(n)
+        cfg = np.array([int(keep_mode), int(mode), int(auto_reset), int(vel_ref), POLICY[policies[0]],
+                        POLICY[policies[1]]], np.int32)
+        self._v = self._L.hkov_create(self.n, cfg, int(seed) & ((1 << 64) - 1), int(arena_offset))
+
+    def close(self):
+        if getattr(self, "_v", None):
+            self._L.hkov_destroy(self._v)
+            self._v = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def reset(self, mask=None, params=None, max_t=None, one_starts=None):
+        c = np.ascontiguousarray
+        m = None if mask is None else c(mask, np.uint8)
+        p = None if params is None else c(params, np.float32)
+        t = None if max_t is None else c(max_t, np.int32)
+        o = None if one_starts is None else c(one_starts, np.uint8)
+        self._L.hkov_reset(self._v, _p(m), _p(p), _p(t), _p(o))
+
+    def set_policy(self, player, policy):
+        self._L.hkov_set_policy(self._v, int(player), POLICY[policy] if isinstance(policy, str) else int(policy))
+
+    def step(self, actions=None, opp_inc=None, with_agent_two=False, final_obs=False):
+        n = self.n
+        a = None if actions is None else np.ascontiguousarray(actions, np.float32).reshape(n, 8)
+        inc = None if opp_inc is None else np.ascontiguousarray(opp_inc, np.float64).reshape(n, 2)
+        out = {"obs": np.zeros((n, 18), np.float32), "reward": np.zeros(n, np.float32),
+               "done": np.zeros(n, np.uint8), "info": np.zeros((n, 4), np.float32),
+               "actions": np.zeros((n, 8), np.float32)}
+        if with_agent_two:
+            out.update(obs2=np.zeros((n, 18), np.float32), reward2=np.zeros(n, np.float32),
+                       info2=np.zeros((n, 4), np.float32))
+        if final_obs:
+            out["final_obs"] = np.zeros((n, 18), np.float32)
+        g = out.get
+        self._L.hkov_step(self._v, _p(a), _p(inc), _p(g("obs")), _p(g("obs2")), _p(g("reward")), _p(g("reward2")),
+                          _p(g("done")), _p(g("info")), _p(g("info2")), _p(g("actions")), _p(g("final_obs")))
+        return out
+
+    def get_state(self):
+        st = np.zeros((self.n, 18), np.float32)
+        aux = np.zeros((self.n, 5), np.int32)
+        self._L.hkov_get_state(self._v, _p(st), _p(aux))
+        return st, aux
+
+    def set_state(self, state=None, aux=None, mask=None):
+        c = np.ascontiguousarray
+        st = None if state is None else c(state, np.float32)
+        ax = None if aux is None else c(aux, np.int32)
+        m = None if mask is None else c(mask, np.uint8)
+        self._L.hkov_set_state(self._v, _p(m), _p(st), _p(ax))
+
+    def observe(self):
+        o, o2 = np.zeros((self.n, 18), np.float32), np.zeros((self.n, 18), np.float32)
+        self._L.hkov_observe(self._v, _p(o), _p(o2))
+        return o, o2
+
+    def phase(self, new=None):
+        out = np.zeros((self.n, 2), np.float64)
+        ph = None if new is None else np.ascontiguousarray(new, np.float64)
+        self._L.hkov_phase(self._v, _p(out), _p(ph))
+        return out
+
+    def counters(self):
+        out = np.zeros(16, np.int64)
+        self._L.hkov_counters(self._v, _p(out))
+        return out
+
+    def time_steps(self, steps, threads=0):
+        """Wall seconds of `steps` batched steps on `threads` OpenMP threads (the CPU baseline)."""
+        return self._L.hkov_time_steps(self._v, int(steps), int(threads))
+
+
+def run_c1(p2_actions, p1_inc, p1_phase0, params, record=True):
+    """BASELINE C1 on one arena, one thread: weak BasicOpponent (player 1) vs the given player-2 actions,
+    reset on done from ``params`` ([E, 6], one row per reset(seed=episode)).  Returns (obs, done, episodes,
+    seconds)."""
+    p2 = np.ascontiguousarray(p2_actions, np.float32)
+    steps = p2.shape[0]
+    inc = np.ascontiguousarray(p1_inc, np.float64)
+    prm = np.ascontiguousarray(params, np.float32)
+    obs = np.zeros((steps, 18), np.float32) if record else None
+    done = np.zeros(steps, np.uint8) if record else None
     sec = ctypes.c_double()
-    pol = {"random": 0, "basic": 1}[policy]
-    total = lib().hko_bench_random(int(n_arenas), int(steps), int(threads), int(seed), pol, ctypes.byref(sec))
-    return int(total), sec.value
+    ep = lib().hko_run_c1(steps, p2, inc, float(p1_phase0), prm, prm.shape[0], _p(obs), _p(done), ctypes.byref(sec))
+    return obs, done, ep, sec.value

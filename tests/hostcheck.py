@@ -45,7 +45,8 @@ def _p(a):
 
 class StepIO(ctypes.Structure):
     _fields_ = [(k, ctypes.c_void_p) for k in ("actions", "opp_inc", "obs", "obs2", "reward", "reward2", "done",
-                                               "info", "info2", "actions_out", "debug")] + [("flags", ctypes.c_int32)]
+                                               "info", "info2", "actions_out", "debug", "final_obs")] + [
+                    ("flags", ctypes.c_int32)]
 
 
 POLICY = {"external": 0, "random": 1, "weak": 2, "strong": 3}
@@ -55,10 +56,10 @@ class HostVec:
     """Same call shapes as hockey_amd.vec_env.VecHockeyEnv for the calls the parity tests make (numpy)."""
 
     def __init__(self, n, keep_mode=True, mode=0, auto_reset=False, vel_ref=False,
-                 policies=("external", "external"), seed=0, arena_offset=0):
+                 policies=("external", "external"), seed=0, arena_offset=0, diag_flags=0):
         self.n = n
         cfg = np.array([int(keep_mode), int(mode), int(auto_reset), int(vel_ref), POLICY[policies[0]],
-                        POLICY[policies[1]]], np.int32)
+                        POLICY[policies[1]], int(diag_flags)], np.int32)
         self._cfg = cfg
         self.L = lib()
         self.h = self.L.hkh_create(n, cfg.ctypes.data, seed, arena_offset)
@@ -82,7 +83,7 @@ class HostVec:
         self.L.hkh_reset(self.h, _p(m), _p(p), _p(mt), None)
 
     def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=False, skip_physics=False,
-             record_actions=False):
+             record_actions=False, final_obs=False):
         n = self.n
         out = SimpleNamespace(obs=np.zeros((n, 18), np.float32), reward=np.zeros(n, np.float32),
                               done=np.zeros(n, np.uint8), info=np.zeros((n, 4), np.float32))
@@ -101,6 +102,9 @@ class HostVec:
         if record_actions:
             out.actions = np.zeros((n, 8), np.float32)
             io.actions_out = _p(out.actions)
+        if final_obs:
+            out.final_obs = np.zeros((n, 18), np.float32)
+            io.final_obs = _p(out.final_obs)
         io.flags = 1 if skip_physics else 0
         self.L.hkh_step(self.h, ctypes.byref(io))
         return out

@@ -264,3 +264,138 @@ def test_rollout_equals_repeated_steps():
         assert np.array_equal(a.counters()[:7], b.counters()[:7])
         a.close()
         b.close()
+
+
+# --------------------------------------------------------------------------------------------- batched contract
+from vec_lockstep import first_mismatch  # noqa: E402
+
+_RES_FIELDS = ("obs", "obs2", "reward", "reward2", "done", "info", "info2", "actions", "final_obs")
+
+
+def _res_np(res, t=None):
+    out = {}
+    for f in _RES_FIELDS:
+        v = getattr(res, f)
+        if v is not None:
+            out[f] = _np(v if t is None else v[t])
+    return out
+
+
+def _bench_path_lockstep(oracle, n, steps, mode, policies, seed, offset=0, diag_flags=0):
+    """GPU (hk_step for the first half, hk_rollout for the rest) vs the oracle's batched context."""
+    env = _vec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset,
+               diag_flags=diag_flags)
+    ov = oracle.OracleVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
+    half = steps // 2
+    for t in range(half):
+        got = _res_np(env.step(None, with_agent_two=True, record_actions=True, final_obs=True))
+        bad = first_mismatch(t, got, ov.step(with_agent_two=True, final_obs=True))
+        if bad:
+            return bad
+    ro = env.rollout(steps - half, with_agent_two=True, record_actions=True, final_obs=True)
+    for t in range(steps - half):
+        bad = first_mismatch(half + t, _res_np(ro, t), ov.step(with_agent_two=True, final_obs=True))
+        if bad:
+            return bad
+    st, aux = env.get_state()
+    ost, oaux = ov.get_state()
+    assert np.array_equal(_np(st), ost) and np.array_equal(_np(aux), oaux)
+    assert np.array_equal(_np(env.opponent_phase()), ov.phase())
+    c, oc = env.counters(), ov.counters()
+    assert np.array_equal(c[:5], oc[:5]), (c[:7], oc[:7])
+    env.close()
+    return {"counters": c}
+
+
+@pytest.mark.parametrize("mode,steps", [(0, 600), (1, 300), (2, 300)])
+def test_bench_path_lockstep_vs_oracle(oracle, mode, steps):
+    """THE benchmarked workload -- strong-vs-strong BasicOpponent fused in the kernel, in-kernel Philox
+    phase increments (opp_inc NULL), auto-reset with device Philox placement -- bit-exact against the
+    oracle's independent restatement, through hk_step and hk_rollout, in all three modes (every arena
+    rolls over at least twice; TRAIN_SHOOTING / TRAIN_DEFENSE device resets included)."""
+    n = 256
+    out = _bench_path_lockstep(oracle, n, steps, mode, ("strong", "strong"), seed=40 + mode)
+    assert "field" not in out, out
+    assert out["counters"][N.CNT_EPISODES] >= 2 * n
+    assert out["counters"][N.CNT_TOI] > 0
+
+
+def test_random_policies_lockstep_vs_oracle(oracle):
+    """C2/C4's random-vs-random Philox actions (and a weak opponent) on a shard with a global offset."""
+    out = _bench_path_lockstep(oracle, 256, 400, 0, ("random", "random"), seed=3, offset=77_000)
+    assert "field" not in out, out
+    out = _bench_path_lockstep(oracle, 128, 300, 1, ("random", "weak"), seed=4, offset=5)
+    assert "field" not in out, out
+
+
+def test_large_island_path_on_gpu_vs_oracle(oracle):
+    """HK_DIAG_LARGE_ISLANDS: every island / TOI mini-island solved on the HBM slot file (the path islands
+    beyond the register slots take in production) -- bit-exact on gfx950 too."""
+    out = _bench_path_lockstep(oracle, 128, 300, 0, ("strong", "strong"), seed=8, diag_flags=N.DIAG_LARGE_ISLANDS)
+    assert "field" not in out, out
+    assert out["counters"][N.CNT_TOI] > 0
+
+
+def test_autoreset_external_policy_transitions(oracle):
+    """auto_reset with an external player: obs after a done step is the NEW episode's first state (so the
+    next action is chosen from it), final_obs holds the terminal observation."""
+    n, steps = 128, 300
+    env = _vec(n, mode=2, policies=("external", "strong"), auto_reset=True, seed=12)
+    ov = oracle.OracleVec(n, mode=2, policies=("external", "strong"), auto_reset=True, seed=12)
+    rng = np.random.default_rng(0)
+    resets = 0
+    for t in range(steps):
+        a = rng.uniform(-1, 1, (n, 8)).astype(np.float32)
+        got = _res_np(env.step(a, with_agent_two=True, record_actions=True, final_obs=True))
+        want = ov.step(a, with_agent_two=True, final_obs=True)
+        assert first_mismatch(t, got, want) is None
+        d = got["done"].astype(bool)
+        resets += int(d.sum())
+        assert np.array_equal(got["obs"][~d], got["final_obs"][~d])
+        if d.any():  # a fresh TRAIN_DEFENSE placement: player 1 at (2, 4) at rest, time 0
+            assert np.all(got["obs"][d, 0:6] == np.array([-3, 0, 0, 0, 0, 0], np.float32))
+    assert resets > n
+    env.close()
+
+
+def test_c4_shard_131072_arenas(oracle):
+    """BASELINE C4's per-GPU shard: 131 072 arenas (random vs random, auto-reset).  Checks: counters and
+    finiteness at full size, 1 x 131 072 == 2 x 65 536 shard contexts with global offsets bit for bit, and
+    three 256-arena blocks (start, middle, end) equal to the oracle run with the same global ids."""
+    n, steps, seed = 131072, 300, 2024
+    full = _vec(n, policies=("random", "random"), auto_reset=True, seed=seed, arena_offset=n)  # rank 1 of C4
+    halves = [_vec(n // 2, policies=("random", "random"), auto_reset=True, seed=seed, arena_offset=n + k * n // 2)
+              for k in range(2)]
+    blocks = (0, n // 2 - 128, n - 256)
+    ovs = [oracle.OracleVec(256, policies=("random", "random"), auto_reset=True, seed=seed, arena_offset=n + b)
+           for b in blocks]
+    for t in range(steps):
+        res = full.step(None, with_agent_two=True, final_obs=True)
+        for h in halves:
+            h.step(None)
+        if t % 25 == 0 or t == steps - 1:  # sampled per-step outputs of the three blocks
+            got = _res_np(res)
+        for b, ov in zip(blocks, ovs):
+            want = ov.step(with_agent_two=True, final_obs=True)
+            if t % 25 == 0 or t == steps - 1:
+                sl = {k: v[b:b + 256] for k, v in got.items()}
+                bad = first_mismatch(t, sl, want)
+                assert bad is None, (b, bad)
+    torch.cuda.synchronize()
+    st, aux = full.get_state()
+    st, aux = _np(st), _np(aux)
+    assert np.isfinite(st).all()
+    for k, h in enumerate(halves):
+        hs, ha = h.get_state()
+        assert np.array_equal(st[k * n // 2:(k + 1) * n // 2], _np(hs))
+        assert np.array_equal(aux[k * n // 2:(k + 1) * n // 2], _np(ha))
+    for b, ov in zip(blocks, ovs):
+        ost, oaux = ov.get_state()
+        assert np.array_equal(st[b:b + 256], ost) and np.array_equal(aux[b:b + 256], oaux)
+    c = full.counters()
+    assert c[N.CNT_STEPS] == n * steps and c[N.CNT_OVERFLOW] == 0
+    assert c[N.CNT_EPISODES] > 0 and c[N.CNT_GOALS_P1] > 0 and c[N.CNT_GOALS_P2] > 0
+    ch = sum(h.counters() for h in halves)
+    assert np.array_equal(c[:7], ch[:7])
+    for e in [full, *halves]:
+        e.close()

@@ -19,9 +19,9 @@ def _f32(x):
     return np.asarray(x, np.float64).astype(np.float32)
 
 
-def _lockstep(oracle, mode, n, steps, seed):
+def _lockstep(oracle, mode, n, steps, seed, **env_kw):
     keep = True
-    env = HostVec(n, keep_mode=keep, mode=mode)
+    env = HostVec(n, keep_mode=keep, mode=mode, **env_kw)
     params = np.zeros((n, 6), np.float32)
     for i in range(n):
         rng, _ = np_random(seed * 100_000 + i)
@@ -72,11 +72,10 @@ def test_kernel_source_lockstep_vs_oracle(oracle, mode, seed):
         assert out["n_toi"] > 0
 
 
-def test_large_island_solver_vs_oracle(oracle, monkeypatch):
-    """HK_ABLATE=1 routes every island / TOI solve through the HBM slot file (HbmSlots, the path of islands
-    with more contacts than the register slots) -- it must be bit-identical as well."""
-    monkeypatch.setenv("HK_ABLATE", "1")
-    out = _lockstep(oracle, 1, n=32, steps=150, seed=3)
+def test_large_island_solver_vs_oracle(oracle):
+    """diag_flags=HK_DIAG_LARGE_ISLANDS routes every island / TOI solve through the HBM slot file (HbmSlots,
+    the path of islands with more contacts than the register slots) -- it must be bit-identical as well."""
+    out = _lockstep(oracle, 1, n=32, steps=150, seed=3, diag_flags=1)
     assert "field" not in out, out
     assert out["counters"][6] > 0  # large-island solves were taken
 
@@ -89,3 +88,44 @@ def test_fused_opponents_autoreset_run(oracle):
     c = env.counters()
     assert c[0] == 256 * 300 and c[5] == 0
     assert c[1] > 0 and c[2] + c[3] <= c[1]
+
+
+# ------------------------------------------------------------------------------------------------ batched contract
+from vec_lockstep import first_mismatch  # noqa: E402
+
+
+def _vec_lockstep(oracle, n, steps, mode, policies, seed, external=False, offset=0):
+    """The kernel source (host build) vs the oracle's batched context on the hk_step contract: fused
+    policies with Philox increments (opp_inc NULL), device auto-reset with episode counters."""
+    env = HostVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
+    ov = oracle.OracleVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
+    rng = np.random.default_rng(seed)
+    for t in range(steps):
+        acts = rng.uniform(-1.2, 1.2, (n, 8)).astype(np.float32) if external else None
+        got = vars(env.step(acts, with_agent_two=True, record_actions=True, final_obs=True))
+        want = ov.step(acts, with_agent_two=True, final_obs=True)
+        bad = first_mismatch(t, got, want)
+        if bad:
+            return bad
+    st, aux = env.get_state()
+    ost, oaux = ov.get_state()
+    assert np.array_equal(st, ost) and np.array_equal(aux, oaux)
+    c, oc = env.counters().astype(np.int64), ov.counters()
+    assert np.array_equal(c[:5], oc[:5]), (c[:7], oc[:7])  # steps, episodes, goals p1 / p2, TOI events
+    return {"counters": c}
+
+
+@pytest.mark.parametrize("mode,steps", [(0, 560), (1, 200), (2, 200)])
+def test_bench_path_vs_oracle_vec(oracle, mode, steps):
+    """The benchmarked workload (strong vs strong, in-kernel Philox phase increments, auto-reset with device
+    placement): every arena rolls over at least twice in every mode."""
+    out = _vec_lockstep(oracle, 64, steps, mode, ("strong", "strong"), seed=5 + mode)
+    assert "field" not in out, out
+    assert out["counters"][1] >= 2 * 64
+
+
+def test_random_and_external_policies_vs_oracle_vec(oracle):
+    out = _vec_lockstep(oracle, 48, 300, 0, ("random", "weak"), seed=21, offset=1000)
+    assert "field" not in out, out
+    out = _vec_lockstep(oracle, 48, 300, 2, ("external", "strong"), seed=22, external=True)
+    assert "field" not in out, out

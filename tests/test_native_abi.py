@@ -35,13 +35,30 @@ def test_library_exports_every_declared_symbol():
     assert b"gfx950" in lib.hk_version()
 
 
-def test_ctypes_struct_layout_matches_header():
+def test_ctypes_struct_layout_matches_header(tmp_path):
+    """Sizes and field offsets of hk_config / hk_step_io as the C compiler lays them out from the header."""
+    import subprocess
+
     from hockey_amd import _native as N
 
-    # hk_config: 4 x int32, int32[2], uint64, int64 -> 40 bytes; hk_step_io: 11 pointers + int32 (padded)
-    assert ctypes.sizeof(N.Config) == 40
-    assert N.Config.seed.offset == 24 and N.Config.arena_offset.offset == 32
-    assert ctypes.sizeof(N.StepIO) == 96 and N.StepIO.flags.offset == 88
+    probes = {"Config": ("hk_config", [f for f, _ in N.Config._fields_]),
+              "StepIO": ("hk_step_io", [f for f, _ in N.StepIO._fields_])}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hockey.h"', "int main(void) {"]
+    for cname, fields in probes.values():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for f in fields:
+            lines.append(f'  printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    want = dict(line.split() for line in subprocess.check_output([str(exe)], text=True).splitlines())
+    for pyname, (cname, fields) in probes.items():
+        S = getattr(N, pyname)
+        assert ctypes.sizeof(S) == int(want[cname]), cname
+        for f in fields:
+            assert getattr(S, f).offset == int(want[f"{cname}.{f}"]), (cname, f)
 
 
 def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
