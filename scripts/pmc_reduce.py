@@ -28,6 +28,7 @@ def per_launch(counter):
 
 if __name__ == "__main__":
     key = sys.argv[1] if len(sys.argv) > 1 else "basic_65536"
+    source = sys.argv[2] if len(sys.argv) > 2 else "scripts/pmc.sh + scripts/pmc_reduce.py"
     fetch_kib, nf = per_launch("FETCH_SIZE")
     write_kib, nw = per_launch("WRITE_SIZE")
     read_b = 2.0 * fetch_kib * 1024.0  # gfx950 FETCH_SIZE correction (x2)
@@ -36,7 +37,7 @@ if __name__ == "__main__":
     d = json.load(open(out_path)) if os.path.exists(out_path) else {}
     d[key] = {"fetch_size_kib_per_launch_raw": fetch_kib, "write_size_kib_per_launch": write_kib,
               "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
-              "hbm_bytes_per_launch": read_b + write_b, "launches": [nf, nw],
+              "hbm_bytes_per_launch": read_b + write_b, "launches": [nf, nw], "source": source,
               "note": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (scripts/pmc.sh); "
                       "FETCH_SIZE x2 per MI355X_MICROARCH.md gfx950 correction"}
     json.dump(d, open(out_path, "w"), indent=1)
