@@ -205,6 +205,14 @@ int hk_observe(void *ctx, float *obs, float *obs2, void *stream) {
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_observe");
 }
 
+int hk_info(void *ctx, double *info, double *info2, double *reward, double *reward2, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_info: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hk::launch_info(c->s, c->cfg, info, info2, reward, reward2, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_info");
+}
+
 int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void *stream) {
   if (!ctx) return fail(HK_E_INVALID, "hk_opponent_phase: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;

@@ -51,6 +51,8 @@ hipError_t launch_reset(const DevState &s, const KCfg &cfg, const uint8_t *mask,
                         const int32_t *max_t, const uint8_t *one, hipStream_t st);
 hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, int nsteps, hipStream_t st);
 hipError_t launch_observe(const DevState &s, const KCfg &cfg, float *obs, float *obs2, hipStream_t st);
+hipError_t launch_info(const DevState &s, const KCfg &cfg, double *info, double *info2, double *reward,
+                       double *reward2, hipStream_t st);
 hipError_t launch_get_state(const DevState &s, const KCfg &cfg, float *state, int32_t *aux, hipStream_t st);
 hipError_t launch_set_state(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *state,
                             const int32_t *aux, hipStream_t st);

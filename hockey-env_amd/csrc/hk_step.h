@@ -377,6 +377,23 @@ HK_DEV void observe_lane(const DevState &s, const KCfg &cfg, int64_t a, float *o
   }
 }
 
+// _get_info / get_info_agent_two / get_reward(_get_info()) / get_reward_agent_two(...) of the current state,
+// float64 like the reference (hockey_env.py:518-591)
+HK_DEV void info_lane(const DevState &s, const KCfg &cfg, int64_t a, double *info, double *info2, double *reward,
+                      double *reward2) {
+  Arena w;
+  load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, nullptr, 0);
+  double i1[4], i2[4];
+  info_side<0>(w, i1);
+  info_side<1>(w, i2);
+  for (int k = 0; k < 4; ++k) {
+    if (info) info[a * 4 + k] = i1[k];
+    if (info2) info2[a * 4 + k] = i2[k];
+  }
+  if (reward) reward[a] = compute_reward(w) + i1[1];
+  if (reward2) reward2[a] = -compute_reward(w) + i2[1];
+}
+
 HK_DEV void get_state_lane(const DevState &s, int64_t a, float *st, int32_t *aux) {
   for (int b = 0; b < 3; ++b) {
     const int o = b * FB;
@@ -398,12 +415,16 @@ HK_DEV void get_state_lane(const DevState &s, int64_t a, float *st, int32_t *aux
   }
 }
 
+// One body's pybox2d setters in set_state's order: position, angle, linearVelocity, angularVelocity
+// (hockey_env.py:595-606).  A NaN entry means "setter not called" (set_state never assigns the puck's angle
+// or angular velocity, :604-605), so a NaN position pair / angle / velocity pair / omega is skipped.
+HK_DEV bool nan_f(float x) { return x != x; }  // IEEE: only a NaN compares unequal to itself (no fast-math)
 template <int B>
 HK_DEV void set_body_state(Arena &w, const float *x) {
-  set_transform<B>(w, V(x[0], x[1]), w.d.a[B]);
-  set_transform<B>(w, V(w.d.px[B], w.d.py[B]), x[2]);
-  set_linear_velocity<B>(w, V(x[3], x[4]));
-  set_angular_velocity<B>(w, x[5]);
+  if (!(nan_f(x[0]) && nan_f(x[1]))) set_transform<B>(w, V(x[0], x[1]), w.d.a[B]);
+  if (!nan_f(x[2])) set_transform<B>(w, V(w.d.px[B], w.d.py[B]), x[2]);
+  if (!(nan_f(x[3]) && nan_f(x[4]))) set_linear_velocity<B>(w, V(x[3], x[4]));
+  if (!nan_f(x[5])) set_angular_velocity<B>(w, x[5]);
 }
 
 // HockeyEnv.set_state (hockey_env.py:594-608) raw form: pybox2d setters, contacts untouched

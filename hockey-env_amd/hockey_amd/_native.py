@@ -41,7 +41,7 @@ class StepIO(ctypes.Structure):
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",
            "hk_step", "hk_rollout", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_observe", "hk_counters",
            "hk_reset_counters",
-           "hk_bytes_per_step"]
+           "hk_bytes_per_step", "hk_info"]
 
 _lib = None
 
@@ -78,13 +78,14 @@ def lib():
     L.hk_get_state.argtypes = [vp, vp, vp, vp]
     L.hk_set_state.argtypes = [vp, vp, vp, vp, vp]
     L.hk_observe.argtypes = [vp, vp, vp, vp]
+    L.hk_info.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hk_opponent_phase.argtypes = [vp, vp, vp, vp]
     L.hk_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), vp]
     L.hk_reset_counters.argtypes = [vp, vp]
     L.hk_bytes_per_step.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     for name in ["hk_create", "hk_destroy", "hk_set_policy", "hk_reset", "hk_step", "hk_rollout", "hk_get_state",
                  "hk_set_state",
-                 "hk_observe", "hk_opponent_phase", "hk_counters", "hk_reset_counters", "hk_bytes_per_step"]:
+                 "hk_observe", "hk_info", "hk_opponent_phase", "hk_counters", "hk_reset_counters", "hk_bytes_per_step"]:
         getattr(L, name).restype = i32
     _lib = L
     return L

@@ -5,19 +5,42 @@ Same names, constructor arguments, return types and quirks as ``hockey/hockey_en
 (:78-81) and the ``Hockey-v0`` / ``Hockey-One-v0`` registrations (:889-903).  Each facade owns a
 one-arena :class:`~hockey_amd.vec_env.VecHockeyEnv`; the step itself always runs on the MI355X.
 
-Documented differences: rewards/info are float32-rounded (the kernel computes them in
-double and emits float32); ``HockeyEnv_BasicOpponent`` evaluates the opponent inside the step kernel
-with a per-arena Philox phase stream instead of the global ``np.random``; ``render`` is out of scope.
+Every value a facade returns is the kernel's: obs / obs_agent_two from hk_step / hk_observe, and info,
+info_agent_two and both rewards from hk_info in float64, exactly as the reference computes them.  One call
+costs the step launch, the info launch and ONE device-to-host copy of a packed output record.  The fused
+``HockeyEnv_BasicOpponent`` opponent draws its phase from the global ``np.random`` exactly like the
+reference's ``BasicOpponent`` (:785, :796), so seeded reference scripts reproduce.  ``render`` is out of scope.
 """
+import ctypes
 import warnings
 
 import numpy as np
 
-from .constants import (CENTER_X, CENTER_Y, FPS, MAX_ANGLE, MAX_TIME_KEEP_PUCK, SCALE, Mode, parse_mode)
+from . import _native as N
+from .constants import CENTER_X, CENTER_Y, FPS, MAX_ANGLE, SCALE, Mode, parse_mode
 from .placement import np_random, placement
 from .spaces import Box, Discrete
 
-__all__ = ["HockeyEnv", "HockeyEnv_BasicOpponent", "BasicOpponent", "Mode", "register_envs", "make"]
+__all__ = ["HockeyEnv", "HockeyEnv_BasicOpponent", "BasicOpponent", "PolicyOpponent", "Mode", "register_envs",
+           "make"]
+
+# packed per-env output record (one device buffer, one D2H copy): byte offsets
+_OBS, _OBS2, _DONE, _INFO, _INFO2, _REW, _REW2, _AUX, _REC = 0, 72, 144, 152, 184, 216, 224, 232, 256
+
+
+def set_state_raw(state, keep_mode=True):
+    """HockeyEnv.set_state (hockey_env.py:594-608) as a raw hk_set_state row: body origins / angles /
+    velocities in float32 as the pybox2d setters store them, NaN where set_state calls no setter (the puck's
+    angle and angular velocity); plus has_puck (int counters) or None when keep_mode is off."""
+    state = np.asarray(state, np.float64)
+    raw = np.full(18, np.nan, np.float32)
+    for b, o in ((0, 0), (1, 6)):
+        raw[6 * b + 0:6 * b + 2] = (state[[o, o + 1]] + [CENTER_X, CENTER_Y]).astype(np.float32)
+        raw[6 * b + 2:6 * b + 6] = state[o + 2:o + 6].astype(np.float32)
+    raw[12:14] = (state[[12, 13]] + [CENTER_X, CENTER_Y]).astype(np.float32)
+    raw[15:17] = state[14:16].astype(np.float32)
+    has = (int(state[16]), int(state[17])) if keep_mode else None
+    return raw, has
 
 
 class HockeyEnv:
@@ -26,6 +49,8 @@ class HockeyEnv:
 
     def __init__(self, keep_mode: bool = True, mode=Mode.NORMAL, verbose: bool = False, device=None,
                  _policies=("external", "external")):
+        import torch
+
         from .vec_env import VecHockeyEnv
 
         self.mode = mode
@@ -33,13 +58,24 @@ class HockeyEnv:
         self.verbose = verbose
         self.seed()
         self._vec = VecHockeyEnv(1, keep_mode=keep_mode, mode=self._mode, device=device, policies=_policies)
+        self._rec = torch.zeros(_REC, dtype=torch.uint8, device=self._vec.device)
+        self._act = torch.zeros(N.ACT_DIM, dtype=torch.float32, device=self._vec.device)
+        self._inc = torch.zeros(2, dtype=torch.float64, device=self._vec.device)
+        base = self._rec.data_ptr()
+        self._io = N.StepIO()
+        self._io.actions = self._act.data_ptr()
+        self._io.obs, self._io.obs2, self._io.done = base + _OBS, base + _OBS2, base + _DONE
+        self._ptr = {k: ctypes.c_void_p(base + off) for k, off in
+                     (("obs", _OBS), ("obs2", _OBS2), ("info", _INFO), ("info2", _INFO2), ("reward", _REW),
+                      ("reward2", _REW2), ("aux", _AUX))}
+        self._snap = None
         self.observation_space = Box(-np.inf, np.inf, shape=(18,), dtype=np.float32)
         self.num_actions = 3 if not self.keep_mode else 4
         self.action_space = Box(-1, +1, (self.num_actions * 2,), dtype=np.float32)
         self.discrete_action_space = Discrete(7)  # sic (hockey_env.py:151): 8 actions are defined
         self.timeStep = 1.0 / FPS
         self.one_starts = True
-        self.max_timesteps = 250 if self._mode == Mode.NORMAL else 80
+        self.max_timesteps = None  # see reset
         self.closest_to_goal_dist = 1000
         self.reset(self.one_starts)
 
@@ -57,6 +93,27 @@ class HockeyEnv:
         self._seed = seed
         return [seed]
 
+    # --------------------------------------------------------------- device record
+    def _refresh(self, stepped):
+        """Fill the packed record for the current state (info / rewards / aux; obs too unless a step just
+        wrote them) and copy it to the host in one transfer."""
+        L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
+        p = self._ptr
+        if not stepped:
+            N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
+        N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
+        N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
+        b = self._rec.cpu().numpy()
+        self._snap = {
+            "obs": np.frombuffer(b, np.float32, 18, _OBS).astype(np.float64),
+            "obs2": np.frombuffer(b, np.float32, 18, _OBS2).astype(np.float64),
+            "done": bool(b[_DONE]), "info": np.frombuffer(b, np.float64, 4, _INFO).copy(),
+            "info2": np.frombuffer(b, np.float64, 4, _INFO2).copy(),
+            "reward": float(np.frombuffer(b, np.float64, 1, _REW)[0]),
+            "reward2": float(np.frombuffer(b, np.float64, 1, _REW2)[0]),
+            "aux": np.frombuffer(b, np.int32, 5, _AUX).copy()}
+        return self._snap
+
     # --------------------------------------------------------------- reset / step
     def reset(self, one_starting=None, mode=None, seed=None, options=None):
         self.seed(seed)
@@ -71,72 +128,62 @@ class HockeyEnv:
         self.closest_to_goal_dist = 1000
         params, max_t = placement(self._mode, self.one_starts, self.np_random)
         self._vec.one_starts[:] = self.one_starts
-        self._vec.reset_params(params[None, :])
-        obs, _ = self._vec.observe()
-        return self._obs_np(obs[0]), self._get_info()
+        # max_t travels explicitly: the kernel's info / time limit follow the mode of THIS reset even after
+        # the mode setter changed it (hockey_env.py:357-365)
+        self._vec.reset_params(params[None, :], max_t=[max_t])
+        s = self._refresh(stepped=False)
+        return self._obs_out(s["obs"]), self._get_info()
+
+    def _launch_step(self, a8, opp_inc=None):
+        self._act.copy_(self._torch_from(a8))
+        io = self._io
+        io.opp_inc = None
+        if opp_inc is not None:
+            self._inc.copy_(self._torch_from(opp_inc))
+            io.opp_inc = self._inc.data_ptr()
+        N.check(self._vec.L.hk_step(self._vec._ctx, ctypes.byref(io), self._vec._stream()), "hk_step")
+        s = self._refresh(stepped=True)
+        return self._obs_out(s["obs"]), s["reward"], s["done"], False, self._info_dict(s["info"])
+
+    @staticmethod
+    def _torch_from(x):
+        import torch
+
+        return torch.from_numpy(np.ascontiguousarray(x))
 
     def step(self, action):
-        a = np.clip(np.asarray(action), -1, +1).astype(np.float32)
+        a = np.clip(np.asarray(action, np.float64), -1, +1).astype(np.float32)  # hockey_env.py:659
         if not self.keep_mode:
             a = np.concatenate([a[0:3], [0.0], a[3:6], [0.0]]).astype(np.float32)
-        res = self._vec.step(a[None, :])
-        obs = self._obs_np(res.obs[0])
-        r = float(res.reward[0].item())
-        d = bool(res.done[0].item())
-        info = self._info_dict(res.info[0].cpu().numpy())
-        return obs, r, d, False, info
+        return self._launch_step(a)
 
     # --------------------------------------------------------------- observations / info
-    def _obs_np(self, t):
-        o = t.cpu().numpy().astype(np.float64)
-        return o if self.keep_mode else o[:16]
+    def _obs_out(self, o):
+        return o.copy() if self.keep_mode else o[:16].copy()
 
     def _get_obs(self):
-        return self._obs_np(self._vec.observe()[0][0])
+        return self._obs_out(self._snap["obs"])
 
     def obs_agent_two(self):
-        return self._obs_np(self._vec.observe()[1][0])
+        return self._obs_out(self._snap["obs2"])
 
     @staticmethod
     def _info_dict(v):
         return {"winner": int(v[0]), "reward_closeness_to_puck": float(v[1]), "reward_touch_puck": float(v[2]),
                 "reward_puck_direction": float(v[3])}
 
-    def _state(self):
-        st, aux = self._vec.get_state()
-        return st[0].cpu().numpy(), aux[0].cpu().numpy()
-
-    def _info_for(self, two):
-        st, aux = self._state()
-        me = st[6:8] if two else st[0:2]
-        puck, pv = st[12:14], st[15:17]
-        T = self.max_timesteps
-        close = 0.0
-        cond = (puck[0] > CENTER_X and pv[0] >= 0) if two else (puck[0] < CENTER_X and pv[0] <= 0)
-        if cond:
-            d = np.asarray(np.float32(me - puck), np.float64)
-            close += float(np.sqrt(np.sum(d ** 2))) * (-30. / (250. / SCALE * T / 2))
-        touch = 1. if aux[1 if two else 0] == MAX_TIME_KEEP_PUCK else 0.
-        f = (-1. if two else 1.) / (T * 25)
-        winner = int(aux[4])
-        return {"winner": -winner if two else winner, "reward_closeness_to_puck": float(close),
-                "reward_touch_puck": float(touch), "reward_puck_direction": float(pv[0]) * f}
-
     def _get_info(self):
-        return self._info_for(False)
+        return self._info_dict(self._snap["info"])
 
     def get_info_agent_two(self):
-        return self._info_for(True)
+        return self._info_dict(self._snap["info2"])
 
     def _compute_reward(self):
-        _, aux = self._state()
-        r = 0
-        if aux[3]:
-            if aux[4] == 1:
-                r += 10
-            elif aux[4] != 0:
-                r -= 10
-        return float(r)
+        """hockey_env.py:518-527 from the kernel's done / winner."""
+        aux = self._snap["aux"]
+        if not aux[3]:
+            return 0.0
+        return 10.0 if aux[4] == 1 else (-10.0 if aux[4] != 0 else 0.0)
 
     def get_reward(self, info):
         return float(self._compute_reward() + info["reward_closeness_to_puck"])
@@ -146,40 +193,34 @@ class HockeyEnv:
 
     # --------------------------------------------------------------- state access (hockey_env.py:594-608)
     def set_state(self, state):
-        state = np.asarray(state, np.float64)
-        st, aux = self._state()
-        raw = st.copy()
-        for b, o in ((0, 0), (1, 6)):
-            raw[6 * b + 0] = np.float32(state[o + 0] + CENTER_X)
-            raw[6 * b + 1] = np.float32(state[o + 1] + CENTER_Y)
-            raw[6 * b + 2:6 * b + 6] = np.float32(state[o + 2:o + 6])
-        raw[12] = np.float32(state[12] + CENTER_X)
-        raw[13] = np.float32(state[13] + CENTER_Y)
-        raw[15] = np.float32(state[14])
-        raw[16] = np.float32(state[15])
-        if self.keep_mode:
-            aux[0], aux[1] = int(state[16]), int(state[17])
+        """pybox2d setters in the reference's order; the puck's angle and angular velocity are not assigned
+        (NaN = setter not called, include/hockey.h hk_set_state).  has_puck is stored as an int counter."""
+        raw, has = set_state_raw(state, self.keep_mode)
+        aux = self._snap["aux"].copy()
+        if has is not None:
+            aux[0], aux[1] = has
         self._vec.set_state(raw[None, :], aux[None, :])
+        self._refresh(stepped=False)
 
     @property
     def time(self):
-        return int(self._state()[1][2])
+        return int(self._snap["aux"][2])
 
     @property
     def done(self):
-        return bool(self._state()[1][3])
+        return bool(self._snap["aux"][3])
 
     @property
     def winner(self):
-        return int(self._state()[1][4])
+        return int(self._snap["aux"][4])
 
     @property
     def player1_has_puck(self):
-        return int(self._state()[1][0])
+        return int(self._snap["aux"][0])
 
     @property
     def player2_has_puck(self):
-        return int(self._state()[1][1])
+        return int(self._snap["aux"][1])
 
     def discrete_to_continous_action(self, discrete_action):
         """hockey_env.py:637-656"""
@@ -245,20 +286,39 @@ class BasicOpponent:
 
 
 class HockeyEnv_BasicOpponent(HockeyEnv):
-    """Hockey-One-v0 (hockey_env.py:875-886): the opponent runs fused inside the GPU step kernel."""
+    """Hockey-One-v0 (hockey_env.py:875-886): the opponent runs fused inside the GPU step kernel on the
+    kernel's own obs_agent_two, with the phase stream of the reference's BasicOpponent: U(0, pi) from the
+    global ``np.random`` at construction (:785) and U(0, 0.2) per act (:796), fed as ``opp_inc``."""
 
     def __init__(self, mode=Mode.NORMAL, weak_opponent=False, device=None):
         super().__init__(mode=mode, keep_mode=True, device=device,
                          _policies=("external", "weak" if weak_opponent else "strong"))
+        self.opponent = BasicOpponent(weak=weak_opponent)  # draws the phase from np.random, as the reference
         self.weak_opponent = weak_opponent
         self.action_space = Box(-1, +1, (4,), dtype=np.float32)
+        self._vec.opponent_phase(np.array([[0.0, self.opponent.phase]]))
 
     def step(self, action):
+        inc = np.random.uniform(0, 0.2)  # the draw opponent.act(obs_agent_two()) makes (hockey_env.py:796)
+        self.opponent.phase += inc       # host mirror of the kernel's phase
         a = np.zeros(8, np.float32)
         a[0:4] = np.clip(np.asarray(action, np.float64)[0:4], -1, 1).astype(np.float32)
-        res = self._vec.step(a[None, :])
-        return (self._obs_np(res.obs[0]), float(res.reward[0].item()), bool(res.done[0].item()), False,
-                self._info_dict(res.info[0].cpu().numpy()))
+        return self._launch_step(a, opp_inc=np.array([0.0, inc]))
+
+
+class PolicyOpponent:
+    """hockey_env.py:908-922: a torch policy as an opponent, ``act(obs) -> np.ndarray`` (4,)."""
+
+    def __init__(self, policy, device=None):
+        self.policy = policy
+        self.device = device
+
+    def act(self, obs):
+        import torch
+
+        with torch.no_grad():
+            x = torch.tensor(obs, dtype=torch.float32, device=self.device).unsqueeze(0)
+            return self.policy(x).squeeze(0).cpu().numpy()
 
 
 _REGISTRY = {

@@ -236,6 +236,17 @@ class VecHockeyEnv:
         N.check(self.L.hk_observe(self._ctx, N.ptr(self.obs_buf), N.ptr(self.obs2_buf), self._stream()), "hk_observe")
         return self.obs_buf, self.obs2_buf
 
+    def info(self):
+        """(info[N,4], info2[N,4], reward[N], reward2[N]) float64 of the current state (hk_info): _get_info,
+        get_info_agent_two and the matching get_reward / get_reward_agent_two of hockey_env.py:518-591."""
+        d, n = self.device, self.n
+        i1 = torch.empty((n, N.INFO_DIM), dtype=torch.float64, device=d)
+        i2 = torch.empty((n, N.INFO_DIM), dtype=torch.float64, device=d)
+        r1 = torch.empty((n,), dtype=torch.float64, device=d)
+        r2 = torch.empty((n,), dtype=torch.float64, device=d)
+        N.check(self.L.hk_info(self._ctx, N.ptr(i1), N.ptr(i2), N.ptr(r1), N.ptr(r2), self._stream()), "hk_info")
+        return i1, i2, r1, r2
+
     def obs_agent_two(self):
         return self.observe()[1]
 

@@ -130,7 +130,9 @@ int hk_step(void *ctx, const hk_step_io *io, void *stream);
 int hk_rollout(void *ctx, int32_t n_steps, const hk_step_io *io, void *stream);
 
 /* Raw state access: state [N,18] f32 (body origins / angles / velocities), aux [N,5] i32.
- * hk_set_state applies pybox2d setter semantics (SetTransform, SetLinearVelocity wakes, ...). */
+ * hk_set_state applies pybox2d setter semantics in set_state's order (SetTransform, SetLinearVelocity wakes,
+ * ...); a NaN position pair / angle / velocity pair / omega leaves that quantity's setter uncalled (the
+ * reference's set_state never assigns the puck's angle or angular velocity, hockey_env.py:594-608). */
 int hk_get_state(void *ctx, float *state, int32_t *aux, void *stream);
 int hk_set_state(void *ctx, const uint8_t *mask, const float *state, const int32_t *aux, void *stream);
 
@@ -140,6 +142,12 @@ int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void
 
 /* Observation of the current state without stepping ([N,18] f32 each, either may be NULL). */
 int hk_observe(void *ctx, float *obs, float *obs2, void *stream);
+
+/* Info dicts and rewards of the current state in float64, as the reference computes them (nullable; info
+ * [N,4] = {winner, closeness, touch, direction}):
+ *   info / info2     replace _get_info / get_info_agent_two            hockey/hockey_env.py:542-591
+ *   reward / reward2 replace get_reward(_get_info()) / get_reward_agent_two(get_info_agent_two())  :518-540 */
+int hk_info(void *ctx, double *info, double *info2, double *reward, double *reward2, void *stream);
 
 /* counters: out[HK_NUM_COUNTERS] int64 on the HOST (synchronises the stream). */
 int hk_counters(void *ctx, int64_t *out, void *stream);

@@ -49,6 +49,7 @@ def lib():
                                          ctypes.c_double, _f64p, _f64p]
         L.hko_stats.argtypes = [ctypes.c_void_p, _i32p]
         L.hko_set_vel_ref.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.hko_begin_contact.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
         L.hko_philox.argtypes = [ctypes.c_uint64, u32p, u32p]
         vp = ctypes.c_void_p
@@ -111,6 +112,9 @@ class OracleWorld:
         d = self._L.hko_step(self._w, np.ascontiguousarray(action8, np.float32), int(skip_physics), obs,
                              ctypes.byref(r), info, dbg)
         return obs, r.value, bool(d), info, dbg
+
+    def begin_contact(self, body_a, body_b):
+        self._L.hko_begin_contact(self._w, int(body_a), int(body_b))
 
     def obs(self):
         o = np.zeros(18, np.float32)

@@ -12,7 +12,9 @@ semantics the reference relies on:
 * ``ApplyForceToCenter`` / ``ApplyTorque`` accumulate float32 forces / torques,
 * ``world.Step`` is a recorded no-op: the Box2D solve itself cannot run here (F1), so these vectors
   pin everything *around* the solve -- reset placement (G1), the pre-solve force laws, hold/shoot and
-  the obs/reward/info/done emission (G2/G3), ``BasicOpponent`` (G4), discrete map + mode parsing (G5).
+  the obs/reward/info/done emission (G2/G3), ``BasicOpponent`` (G4), discrete map + mode parsing (G5),
+  G2 under the live-reference velocity getter (G2R), ``ContactDetector.BeginContact`` on
+  fake contacts (G7) and ``set_state`` (G8).
 
 Mass properties (G6) come from a float32 restatement of Box2D 2.3 ``b2PolygonShape::Set`` /
 ``ComputeMass`` / ``b2Body::ResetMassData`` written here with numpy float32 scalars; the reference
@@ -593,6 +595,105 @@ def gen_g5(he):
                         act_shape_nokeep=np.array(envn.action_space.shape))
 
 
+def gen_g2r(he, n=3000, seed=1234):
+    """G2 under the Q1 "live reference" reading of pybox2d's velocity getter: the vector
+    ``player.linearVelocity`` returns writes through to the body, so _check_boundaries' ``[i] = 0`` zeroes the
+    velocity and the force becomes -0.  Same sampled cases as G2 (same seed), fewer of them."""
+    orig = FakeBody.linearVelocity
+    FakeBody.linearVelocity = property(lambda s: s._v, orig.fset)  # live vector: __setitem__ hits the body
+    try:
+        out = os.path.join(OUT, "g2_step_presolve.npz")
+        tmp = os.path.join(OUT, "_g2r_tmp.npz")
+        os.replace(out, out + ".keep")
+        try:
+            gen_g2(he, n=n, seed=seed)
+            os.replace(out, tmp)
+        finally:
+            os.replace(out + ".keep", out)
+        os.replace(tmp, os.path.join(OUT, "g2r_step_presolve_live.npz"))
+    finally:
+        FakeBody.linearVelocity = orig
+    return n
+
+
+# body ids of the oracle / kernel scene (oracle/hk_oracle.c enum B_*): p1, p2, puck, top wall, goal 1, goal 2
+G7_BODIES = {"player1": 0, "player2": 1, "puck": 2, "wall": 3, "goal_player_1": 9, "goal_player_2": 10}
+
+
+def gen_g7(he):
+    """ContactDetector.BeginContact (hockey_env.py:44-76) on fake contacts: every ordered body pair x puck vx
+    around the +-0.1 thresholds x has_puck x keep_mode x prior done / winner."""
+    from types import SimpleNamespace as NS
+
+    rows = {k: [] for k in ["keep", "body_a", "body_b", "puck_vx", "has_in", "dw_in", "has_out", "dw_out"]}
+    vxs = [-5.0, -0.2, -0.1, float(f32(-0.1)), -0.0999, 0.0, 0.0999, 0.1, float(f32(0.1)), 0.1001, 0.2, 5.0]
+    for keep in (True, False):
+        env = he.HockeyEnv(keep_mode=keep)
+        cd = he.ContactDetector(env)
+        bodies = {"player1": env.player1, "player2": env.player2, "puck": env.puck, "wall": env.world_objects[-1],
+                  "goal_player_1": env.goal_player_1, "goal_player_2": env.goal_player_2}
+        for na, ba in bodies.items():
+            for nb, bb in bodies.items():
+                if na == nb:
+                    continue
+                for vx in vxs:
+                    for h1, h2 in ((0, 0), (0, 7), (5, 0), (15, 15)):
+                        for d0, w0 in ((0, 0), (1, -1), (1, 1)):
+                            env.puck._v = FakeVec(vx, 0.3)
+                            env.player1_has_puck, env.player2_has_puck = h1, h2
+                            env.done, env.winner = bool(d0), w0
+                            cd.BeginContact(NS(fixtureA=NS(body=ba), fixtureB=NS(body=bb)))
+                            rows["keep"].append(int(keep))
+                            rows["body_a"].append(G7_BODIES[na])
+                            rows["body_b"].append(G7_BODIES[nb])
+                            rows["puck_vx"].append(f32(vx))
+                            rows["has_in"].append([h1, h2])
+                            rows["dw_in"].append([d0, w0])
+                            rows["has_out"].append([int(env.player1_has_puck), int(env.player2_has_puck)])
+                            rows["dw_out"].append([int(env.done), int(env.winner)])
+    np.savez_compressed(os.path.join(OUT, "g7_begin_contact.npz"),
+                        **{k: np.array(v, np.float32 if k == "puck_vx" else np.int32) for k, v in rows.items()})
+    return len(rows["keep"])
+
+
+def gen_g8(he, n=400, seed=77):
+    """HockeyEnv.set_state (hockey_env.py:594-608) on an obs-format vector: the bodies' float32 setter results,
+    has_puck, and the observation that follows."""
+    rng = np.random.default_rng(seed)
+    rows = {k: [] for k in ["keep", "state", "raw_after", "has_after", "obs_after", "raw_before"]}
+    for i in range(n):
+        keep = bool(i % 4 != 3)
+        env = he.HockeyEnv(keep_mode=keep)
+        env.puck._a, env.puck._w = f32(rng.uniform(-3, 3)), f32(rng.uniform(-9, 9))  # untouched by set_state
+        before = body_state(env.player1) + body_state(env.player2) + body_state(env.puck)
+        st = np.zeros(18)
+        st[0:2] = rng.uniform([-4.2, -3.2], [4.2, 3.2])
+        st[2] = rng.uniform(-1.5, 1.5)
+        st[3:6] = rng.uniform(-12, 12, 3)
+        st[6:8] = rng.uniform([-4.2, -3.2], [4.2, 3.2])
+        st[8] = rng.uniform(-1.5, 1.5)
+        st[9:12] = rng.uniform(-12, 12, 3)
+        st[12:14] = rng.uniform([-4.7, -3.7], [4.7, 3.7])
+        st[14:16] = rng.uniform(-30, 30, 2)
+        st[16:18] = rng.choice([0, 0, 3, 14, 15], 2)
+        if rng.random() < 0.2:
+            st[:16] = np.round(st[:16], 1)  # decimal inputs: the float64 -> float32 rounding paths
+        env.set_state(st if keep else st.copy())
+        rows["keep"].append(int(keep))
+        rows["state"].append(st)
+        rows["raw_before"].append(before)
+        rows["raw_after"].append(body_state(env.player1) + body_state(env.player2) + body_state(env.puck))
+        rows["has_after"].append([float(env.player1_has_puck), float(env.player2_has_puck)])
+        obs = np.asarray(env._get_obs(), np.float64)
+        rows["obs_after"].append(obs if keep else np.concatenate([obs, [0, 0]]))
+    np.savez_compressed(os.path.join(OUT, "g8_set_state.npz"), keep=np.array(rows["keep"], np.int32),
+                        state=np.array(rows["state"], np.float64), raw_before=np.array(rows["raw_before"], np.float32),
+                        raw_after=np.array(rows["raw_after"], np.float32),
+                        has_after=np.array(rows["has_after"], np.float64),
+                        obs_after=np.array(rows["obs_after"], np.float64))
+    return n
+
+
 def main():
     he = load_reference()
     geo = geometry(he)
@@ -605,6 +706,9 @@ def main():
     print("G2 rows", gen_g2(he))
     print("G4 rows", gen_g4(he))
     gen_g5(he)
+    print("G2R rows", gen_g2r(he))
+    print("G7 rows", gen_g7(he))
+    print("G8 rows", gen_g8(he))
     print("done ->", OUT)
 
 

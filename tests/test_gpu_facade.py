@@ -1,0 +1,290 @@
+"""GPU tests of the drop-in surfaces: the gymnasium facades (Hockey-v0 / Hockey-One-v0) against the reference-
+generated goldens and the oracle, the Q1 live-reference variant through the kernel, BeginContact scenarios, the
+BASELINE C1 protocol, and the reference's own stage-3 actor under the reference's evaluation protocol.
+
+Every facade value is compared exactly: obs as float64 of the kernel's float32, rewards and info in float64
+(hk_info computes them in double like the reference)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from hockey_amd import _native as N  # noqa: E402
+from hockey_amd.placement import np_random, placement  # noqa: E402
+
+INFO_KEYS = ("winner", "reward_closeness_to_puck", "reward_touch_puck", "reward_puck_direction")
+
+
+def _vec(n, keep=True, mode=0, **kw):
+    from hockey_amd.vec_env import VecHockeyEnv
+    return VecHockeyEnv(n, keep_mode=keep, mode=mode, device="cuda:0", **kw)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _info_vec(d):
+    return np.array([d[k] for k in INFO_KEYS], np.float64)
+
+
+# ------------------------------------------------------------------------------------------------ goldens
+def test_facade_g2_step_laws_exact(golden):
+    """Hockey-v0 facade on every G2 case (keep_mode on and off, all modes): obs, obs_agent_two, float64 reward
+    and info dicts, get_reward_agent_two(get_info_agent_two()), done, time -- equal to the reference's."""
+    from hockey_amd.hockey_env import HockeyEnv
+
+    g2 = golden("g2_step_presolve.npz")
+    envs = {}
+    bad = {}
+    for i in range(len(g2["mode"])):
+        keep, mode = bool(g2["keep_mode"][i]), int(g2["mode"][i])
+        if (keep, mode) not in envs:
+            e = HockeyEnv(keep_mode=keep, mode=mode)
+            e._io.flags = N.STEP_SKIP_PHYSICS  # world.Step as a no-op, as in the golden harness
+            envs[(keep, mode)] = e
+        env = envs[(keep, mode)]
+        env._vec.set_state(g2["state"][i][None, :], g2["aux"][i][None, :])
+        env._refresh(stepped=False)
+        act = g2["action"][i]
+        a = act if keep else np.concatenate([act[0:3], act[4:7]])
+        obs, r, d, trunc, info = env.step(a)
+        k = 18 if keep else 16
+        checks = {"obs": np.array_equal(obs, g2["obs"][i][:k]), "reward": r == g2["reward"][i],
+                  "done": int(d) == g2["done"][i], "trunc": trunc is False,
+                  "info": np.array_equal(_info_vec(info), g2["info"][i]),
+                  "obs2": np.array_equal(env.obs_agent_two(), g2["obs2"][i][:k]),
+                  "info2": np.array_equal(_info_vec(env.get_info_agent_two()), g2["info2"][i]),
+                  "reward2": env.get_reward_agent_two(env.get_info_agent_two()) == g2["reward2"][i],
+                  "reward_fn": env.get_reward(info) == g2["reward"][i],
+                  "time": env.time == g2["has_after"][i][2],
+                  "has": (env.player1_has_puck, env.player2_has_puck) == tuple(g2["has_after"][i][:2])}
+        for f, ok in checks.items():
+            if not ok:
+                bad.setdefault(f, []).append(i)
+    for e in envs.values():
+        e.close()
+    assert not bad, {k: v[:5] for k, v in bad.items()}
+
+
+def test_kernel_g2r_live_reference_semantics(golden):
+    """vel_ref_semantics=1 (SURVEY App. B Q1 "live reference") through the kernel == G2R bit for bit."""
+    g2r = golden("g2r_step_presolve_live.npz")
+    bad = {}
+    for keep in (True, False):
+        for mode in (0, 1, 2):
+            idx = np.nonzero((g2r["keep_mode"] == int(keep)) & (g2r["mode"] == mode))[0]
+            if len(idx) == 0:
+                continue
+            n = len(idx)
+            env = _vec(n, keep=keep, mode=mode, vel_ref_semantics=True)
+            env.reset_params(np.tile(np.array([8, 4, 3, 4, 0, 0], np.float32), (n, 1)))
+            env.set_state(g2r["state"][idx], g2r["aux"][idx])
+            dbg = torch.zeros((n, N.DEBUG_DIM), dtype=torch.float32, device="cuda:0")
+            res = env.step(g2r["action"][idx], with_agent_two=True, debug=dbg, skip_physics=True)
+            st, aux = env.get_state()
+            i1, i2, r1, r2 = env.info()
+            d = _np(dbg)
+            got = {"force": d[:, 0:6].reshape(n, 3, 2), "torque": d[:, 6:8], "ldamp": d[:, 8:11],
+                   "adamp": d[:, 11:13], "state_after": _np(st), "has_after": _np(aux)[:, 0:3],
+                   "obs": _np(res.obs).astype(np.float64), "obs2": _np(res.obs2).astype(np.float64),
+                   "done": _np(res.done).astype(np.int32), "info": _np(i1), "info2": _np(i2),
+                   "reward": _np(r1), "reward2": _np(r2)}
+            for f, v in got.items():
+                ok = np.all(v.reshape(n, -1) == g2r[f][idx].reshape(n, -1), axis=1)
+                if not ok.all():
+                    bad.setdefault(f, []).extend(idx[~ok][:3].tolist())
+            env.close()
+    assert not bad, bad
+
+
+def test_facade_set_state_g8(golden):
+    """HockeyEnv.set_state through the facade: the bodies the reference's pybox2d setters leave, has_puck and
+    the next observation (G8); the puck's angle and angular velocity stay untouched."""
+    from hockey_amd.hockey_env import HockeyEnv
+
+    g8 = golden("g8_set_state.npz")
+    envs = {k: HockeyEnv(keep_mode=bool(k)) for k in (0, 1)}
+    for i in range(len(g8["keep"])):
+        keep = bool(g8["keep"][i])
+        env = envs[int(keep)]
+        env._vec.set_state(g8["raw_before"][i][None, :], np.zeros((1, 5), np.int32))
+        env._refresh(stepped=False)
+        env.set_state(g8["state"][i])
+        st, _ = env._vec.get_state()
+        assert np.array_equal(_np(st)[0], g8["raw_after"][i]), i
+        k = 18 if keep else 16
+        assert np.array_equal(env._get_obs(), g8["obs_after"][i][:k]), i
+        if keep:
+            assert (env.player1_has_puck, env.player2_has_puck) == tuple(g8["has_after"][i].astype(int)), i
+
+
+# ------------------------------------------------------------------------------------------------ BeginContact
+def test_begin_contact_scenarios(oracle):
+    """Goal right / goal left / possession by player 1 and 2 (and a puck too fast for possession): set_state
+    plus steps through the kernel, equal to the oracle, with the outcome ContactDetector.BeginContact
+    prescribes (G7 pins that listener against the reference)."""
+    base = np.array([2, 4, 0, 0, 0, 0, 8, 4, 0, 0, 0, 0, 5, 4, 0, 0, 0, 0], np.float32)
+    scen = {  # puck x, y, vx -> expected (done, winner, has1, has2) after the first step
+        "goal_right": ((9.25, 4.0, 0.0), (1, 1, 0, 0)), "goal_left": ((0.75, 4.0, 0.0), (1, -1, 0, 0)),
+        "p1_catch": ((2.3, 4.0, 0.0), (0, 0, 15, 0)), "p2_catch": ((7.7, 4.0, 0.0), (0, 0, 0, 15)),
+        "p1_too_fast": ((2.3, 4.0, 0.5), (0, 0, 0, 0)), "p2_too_fast": ((7.7, 4.0, -0.5), (0, 0, 0, 0))}
+    n = len(scen)
+    states = np.tile(base, (n, 1))
+    for k, ((x, y, vx), _) in enumerate(scen.values()):
+        states[k, 12:16] = [x, y, 0, vx]
+    aux = np.zeros((n, 5), np.int32)
+    env = _vec(n)
+    env.reset_params(np.tile(np.array([8, 4, 5, 4, 0, 0], np.float32), (n, 1)))
+    env.set_state(states, aux)
+    ws = []
+    for k in range(n):
+        w = oracle.OracleWorld(True, 0)
+        w.reset(np.array([8, 4, 5, 4, 0, 0], np.float32), 250)
+        w.set_raw(states[k], aux[k])
+        ws.append(w)
+    zero = np.zeros((n, 8), np.float32)
+    for t in range(3):
+        res = env.step(zero)
+        st, ax = env.get_state()
+        for k, w in enumerate(ws):
+            o, r, d, info, _ = w.step(zero[k])
+            assert np.array_equal(_np(res.obs)[k], o) and bool(_np(res.done)[k]) == d, (t, k)
+            wst, wax = w.get_raw()
+            assert np.array_equal(_np(st)[k], wst) and np.array_equal(_np(ax)[k], wax), (t, k)
+        if t == 0:
+            a = _np(ax)
+            for k, (name, (_, (dn, win, h1, h2))) in enumerate(scen.items()):
+                assert (a[k, 3], a[k, 4], a[k, 0], a[k, 1]) == (dn, win, h1, h2), (name, a[k])
+    env.close()
+
+
+# ------------------------------------------------------------------------------------------------ facade runs
+def test_facade_mode_switch_then_episode(oracle):
+    """The reference's only working mode change is the setter (reset(mode=...) raises): after
+    ``env.mode = 'TRAIN_DEFENSE'`` the next reset places a TRAIN_DEFENSE arena with max_timesteps 80, and the
+    episode's info / reward / time limit use T = 80 (the kernel used to keep T = 250)."""
+    from hockey_amd.hockey_env import HockeyEnv
+
+    env = HockeyEnv()
+    env.mode = "TRAIN_DEFENSE"
+    obs, info = env.reset(seed=3)
+    assert env.max_timesteps == 80
+    rng, _ = np_random(3)
+    params, max_t = placement(2, env.one_starts, rng)
+    w = oracle.OracleWorld(True, 2)
+    w.reset(params, max_t)
+    assert np.array_equal(obs, w.obs().astype(np.float64))
+    act = np.random.default_rng(5).uniform(-1, 1, (81, 8)).astype(np.float32)
+    for t in range(81):
+        obs, r, d, _, info = env.step(act[t])
+        o, wr, wd, winfo, _ = w.step(act[t])
+        assert np.array_equal(obs, o.astype(np.float64)) and r == wr and d == wd, t
+        assert np.array_equal(_info_vec(info), winfo), t
+        if t < 80 and not wd:
+            assert not d
+    assert d and env.time == 81
+    env.close()
+
+
+def test_c1_protocol_facade_vs_oracle(oracle):
+    """BASELINE C1 through the Hockey-v0 facade: BasicOpponent(weak) from hockey_amd (host, global
+    np.random phase stream) vs U(-1,1) from default_rng(0), reset(seed=episode) on done, 10 000 steps -- the
+    observation sequence equals the oracle's run of the same protocol."""
+    from hockey_amd.hockey_env import BasicOpponent, HockeyEnv
+
+    steps = 10_000
+    np.random.seed(0)
+    p1 = BasicOpponent(weak=True)
+    p2 = np.random.default_rng(0).uniform(-1, 1, (steps, 4))
+    env = HockeyEnv()
+    ep = 0
+    obs, _ = env.reset(seed=ep)
+    got = np.zeros((steps, 18))
+    for t in range(steps):
+        a = np.hstack([p1.act(obs), p2[t]])
+        obs, r, d, _, info = env.step(a)
+        got[t] = obs
+        if d:
+            ep += 1
+            obs, _ = env.reset(seed=ep)
+    env.close()
+    legacy = np.random.RandomState(0)
+    phase0 = legacy.uniform(0, np.pi)
+    inc = legacy.uniform(0, 0.2, steps)
+    params, one = [], True
+    for e in range(ep + 1):
+        one = not one
+        rng, _ = np_random(e)
+        params.append(placement(0, one, rng)[0])
+    want, _, n_ep, _ = oracle.run_c1(p2.astype(np.float32), inc, phase0, np.stack(params))
+    assert n_ep == ep + 1
+    bad = np.nonzero(~np.all(got == want.astype(np.float64), axis=1))[0]
+    assert len(bad) == 0, (int(bad[0]), got[bad[0]], want[bad[0]])
+    assert ep >= 20
+
+
+def test_hockey_one_seeded_run_vs_oracle(oracle):
+    """Hockey-One-v0 reproduces a seeded reference run: the fused opponent takes the global np.random phase
+    stream of the reference's BasicOpponent (init U(0, pi), U(0, 0.2) per act), so with np.random.seed(s) the
+    facade equals the oracle driven by the same stream -- obs, float64 reward and info, done."""
+    from hockey_amd.hockey_env import HockeyEnv_BasicOpponent
+
+    np.random.seed(5)
+    env = HockeyEnv_BasicOpponent(weak_opponent=False)
+    legacy = np.random.RandomState(5)
+    phase = legacy.uniform(0, np.pi)
+    assert env.opponent.phase == phase
+    seed = 11
+    obs, _ = env.reset(seed=seed)
+    rng, _ = np_random(seed)
+    params, max_t = placement(0, env.one_starts, rng)
+    w = oracle.OracleWorld(True, 0)
+    w.reset(params, max_t)
+    acts = np.random.default_rng(1).uniform(-1, 1, (600, 4))
+    episodes = 0
+    for t in range(600):
+        inc = legacy.uniform(0, 0.2)
+        a2, phase = oracle.basic_opponent(0, 1, phase, inc, w.obs_two().astype(np.float64))
+        obs, r, d, _, info = env.step(acts[t])
+        o, wr, wd, winfo, _ = w.step(np.concatenate([np.clip(acts[t], -1, 1), a2]).astype(np.float32))
+        assert np.array_equal(obs, o.astype(np.float64)) and r == wr and d == wd, t
+        assert np.array_equal(_info_vec(info), winfo), t
+        if d:
+            episodes += 1
+            seed += 1
+            obs, _ = env.reset(seed=seed)
+            rng, _ = np_random(seed)
+            params, max_t = placement(0, env.one_starts, rng)
+            w.reset(params, max_t)
+    assert episodes >= 2
+    assert env.opponent.phase == phase
+    env.close()
+
+
+# ------------------------------------------------------------------------------------------------ behaviour
+def test_stage3_actor_reproduces_recorded_win_rates(golden):
+    """The reference's stage-3 best actor (pretrained/stage_3/models/td3_best.pt, extracted weights-only into
+    tests/golden/stage3_actor.npz) under the reference's evaluation protocol (rl/utils/evaluator.py:10-35:
+    Hockey-One-v0, reset seeds 42..141, greedy actions): win rates within 3 binomial standard errors of the
+    recorded WR_strong / WR_weak (metrics.json eval 53).  The GPU arenas restate Box2D (parity unpinned per
+    trajectory) and draw the opponent phase per arena: this is the behavioural pin."""
+    from hockey_amd.evaluate import Actor, evaluate
+
+    z = golden("stage3_actor.npz")
+    actor = Actor().to("cuda:0")
+    with torch.no_grad():
+        for name, p in actor.named_parameters():
+            p.copy_(torch.from_numpy(z[name.replace(".", "_")]))
+    actor.eval()
+    n = int(z["eval_episodes"])
+    for weak, rec in ((False, float(z["wr_strong"])), (True, float(z["wr_weak"]))):
+        r = evaluate(actor, episodes=n, seed=int(z["eval_seed"]), weak_opponent=weak)
+        big = evaluate(actor, episodes=4000, seed=int(z["eval_seed"]), weak_opponent=weak)
+        p = big["win"]
+        se = np.sqrt(max(p * (1 - p), 0.01 * 0.99) / n)  # the recorded rate is itself a 100-episode estimate
+        print(f"stage3 actor vs {'weak' if weak else 'strong'}: WR {r['win']:.3f} (100 eps), {p:.4f} (4000 eps), "
+              f"recorded {rec}")
+        assert abs(rec - p) <= 3 * se, (weak, rec, p, r)

@@ -132,3 +132,71 @@ def test_oracle_mirror_symmetry(oracle, keep):
         assert np.array_equal(o2[0:2], -o[6:8]) and np.array_equal(o2[6:8], -o[0:2])
         assert np.array_equal(o2[3:5], -o[9:11]) and np.array_equal(o2[12:16], -o[12:16])
         assert o2[2] == o[8] and o2[8] == o[2] and o2[16] == o[17] and o2[17] == o[16]
+
+
+def test_g2r_live_reference_velocity_bit_exact(oracle, golden):
+    """SURVEY App. B Q1, "live reference" reading: _check_boundaries' ``player.linearVelocity[i] = 0`` writes
+    through to the body (G2R, generated with a write-through velocity getter)."""
+    g2r = golden("g2r_step_presolve_live.npz")
+    worlds = {(k, m): oracle.OracleWorld(k, m, vel_ref=True) for k in (True, False) for m in (0, 1, 2)}
+    bad = {}
+    for i in range(len(g2r["mode"])):
+        got = _run_g2_case(oracle, g2r, i, worlds)
+        for f in G2_FIELDS:
+            if not np.array_equal(np.asarray(got[f]), g2r[f][i]):
+                bad.setdefault(f, []).append(i)
+    assert not bad, {k: v[:5] for k, v in bad.items()}
+
+
+def test_g2r_differs_from_copy_semantics(golden):
+    """The two Q1 readings are distinguishable on these cases (zeroed velocities, -0 boundary forces)."""
+    g2, g2r = golden("g2_step_presolve.npz"), golden("g2r_step_presolve_live.npz")
+    n = len(g2r["mode"])
+    assert np.array_equal(g2["state"][:n], g2r["state"]) and np.array_equal(g2["action"][:n], g2r["action"])
+    moved = ~np.all(g2["state_after"][:n] == g2r["state_after"], axis=1)
+    assert moved.sum() > 100
+
+
+def test_g7_begin_contact(oracle, golden):
+    """ContactDetector.BeginContact (hockey_env.py:44-76): every ordered body pair, puck vx around the +-0.1
+    possession thresholds (float32 vx compared in double), has_puck, keep_mode and prior done / winner."""
+    g7 = golden("g7_begin_contact.npz")
+    worlds = {k: oracle.OracleWorld(bool(k), 0) for k in (0, 1)}
+    for i in range(len(g7["keep"])):
+        w = worlds[int(g7["keep"][i])]
+        st, aux = w.get_raw()
+        st[15] = g7["puck_vx"][i]
+        aux[0], aux[1] = g7["has_in"][i]
+        aux[3], aux[4] = g7["dw_in"][i]
+        w.set_raw(st, aux)
+        w.begin_contact(g7["body_a"][i], g7["body_b"][i])
+        _, aux = w.get_raw()
+        assert list(aux[[0, 1]]) == list(g7["has_out"][i]) and list(aux[[3, 4]]) == list(g7["dw_out"][i]), i
+    # coverage: goals both ways, both possession triggers and their thresholds
+    assert ((g7["dw_out"][:, 1] == 1) & (g7["dw_in"][:, 1] != 1)).any()
+    assert ((g7["dw_out"][:, 1] == -1) & (g7["dw_in"][:, 1] != -1)).any()
+    assert ((g7["has_out"][:, 0] == 15) & (g7["has_in"][:, 0] == 0)).sum() > 0
+    assert ((g7["has_out"][:, 1] == 15) & (g7["has_in"][:, 1] == 0)).sum() > 0
+
+
+def test_g8_set_state(oracle, golden):
+    """HockeyEnv.set_state on an obs-format vector: hockey_amd's conversion (the rows the facade hands to
+    hk_set_state, NaN = setter not called) applied with pybox2d setter semantics gives the reference's bodies,
+    has_puck and next observation."""
+    from hockey_amd.hockey_env import set_state_raw
+
+    g8 = golden("g8_set_state.npz")
+    for i in range(len(g8["keep"])):
+        keep = bool(g8["keep"][i])
+        w = oracle.OracleWorld(keep, 0)
+        w.set_raw(g8["raw_before"][i], np.zeros(5, np.int32))
+        raw, has = set_state_raw(g8["state"][i], keep)
+        aux = np.zeros(5, np.int32)
+        if has is not None:
+            aux[0], aux[1] = has
+        w.set_raw(raw, aux)
+        st, ax = w.get_raw()
+        assert np.array_equal(st, g8["raw_after"][i]), i
+        if keep:
+            assert list(ax[[0, 1]]) == list(g8["has_after"][i].astype(int)), i
+        assert np.array_equal(w.obs().astype(np.float64), g8["obs_after"][i]), i
