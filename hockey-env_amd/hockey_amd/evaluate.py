@@ -104,3 +104,80 @@ def evaluate(policy, episodes=100, seed=42, weak_opponent=False, mode=Mode.NORMA
     return {"episodes": episodes, "win": float((w == 1).mean()), "draw": float((w == 0).mean()),
             "loss": float((w == -1).mean()), "mean_return": float(ret.mean().item()),
             "mean_length": float(length.double().mean().item())}
+
+
+# Hockey-Env.ipynb:940-2154 (cells 51-57): 1000 strong-vs-strong BasicOpponent games, unseeded resets on one
+# reused env, up to 500 steps with a break at done.  Recorded: 150 911 steps, winners +1/0/-1 = 319/368/313,
+# sum of rewards -4360.24 (agent 1) / -4367.87 (agent 2), and the per-feature mean of every step's obs.
+NOTEBOOK_STUDY = {
+    "games": 1000, "steps": 150911, "win": 0.319, "draw": 0.368, "loss": 0.313,
+    "reward_sum": -4360.24, "reward2_sum": -4367.87,
+    "obs_mean": [-2.9737481, -0.00389052, -0.00098744, -0.06068974, 0.00053737, 0.00684031, 2.96906086,
+                 0.00154943, -0.0013995, 0.0559986, -0.00210782, -0.00475535, -0.0208698, -0.0031277,
+                 0.01032396, 0.00961799, 1.10906428, 1.10767273]}
+
+
+@torch.no_grad()
+def basic_vs_basic_study(games, seed=0, vel_ref_semantics=False, device="cuda:0"):
+    """The notebook's strong-vs-strong study on ``games`` arenas (one game each, resets alternating the puck side
+    like the reused reference env, opponent phases uniform mod 2 pi like its long-lived opponents), with per-game
+    statistics for standard errors: winner, length, return of
+    both agents and the per-game sum of obs.  Returns a dict of numpy arrays."""
+    from .vec_env import VecHockeyEnv
+
+    env = VecHockeyEnv(games, keep_mode=True, device=device, policies=("strong", "strong"), auto_reset=False,
+                       seed=seed, vel_ref_semantics=vel_ref_semantics)
+    params, max_t, _ = reset_params(games, seed)
+    env.reset_params(params)
+    # the notebook's two BasicOpponent objects live across all 1000 games, so a game starts wherever the phase
+    # walk (U(0, 0.2) per step) has got to: uniform mod 2 pi, not the U(0, pi) of a fresh BasicOpponent
+    env.opponent_phase(np.random.default_rng(seed).uniform(0, 2 * np.pi, (games, 2)))
+    dev = env.device
+    live = torch.ones(games, dtype=torch.bool, device=dev)
+    ret = torch.zeros(games, dtype=torch.float64, device=dev)
+    ret2 = torch.zeros(games, dtype=torch.float64, device=dev)
+    length = torch.zeros(games, dtype=torch.int64, device=dev)
+    winner = torch.zeros(games, dtype=torch.float32, device=dev)
+    obs_sum = torch.zeros((games, 18), dtype=torch.float64, device=dev)
+    for _ in range(max_t + 1):
+        res = env.step(None, with_agent_two=True)
+        lv = live.double()
+        ret += lv * res.reward.double()
+        ret2 += lv * res.reward2.double()
+        obs_sum += lv[:, None] * res.obs.double()
+        length += live.long()
+        d = res.done.bool()
+        winner = torch.where(live & d, res.info[:, 0], winner)
+        live &= ~d
+        if not bool(live.any()):
+            break
+    env.close()
+    return {"winner": winner.cpu().numpy(), "length": length.cpu().numpy(), "return": ret.cpu().numpy(),
+            "return2": ret2.cpu().numpy(), "obs_sum": obs_sum.cpu().numpy()}
+
+
+def study_zscores(per_game, ref=NOTEBOOK_STUDY):
+    """z-scores of a per-game study against the notebook's 1000 games, with the combined standard error of both
+    estimates (the notebook's own error estimated from this study's between-game spread at n = 1000; obs means
+    by the ratio estimator sum(obs) / sum(steps) with per-game clustering)."""
+    w, L = per_game["winner"], per_game["length"].astype(np.float64)
+    n, m = len(w), ref["games"]
+    out = {"games": n}
+
+    def z(est, ref_val, var1):  # var1 = variance of one game's contribution
+        se = np.sqrt(var1 / n + var1 / m)
+        return {"value": float(est), "notebook": float(ref_val), "se_combined": float(se),
+                "z": float((est - ref_val) / se) if se > 0 else 0.0}
+
+    for key, val in (("win", 1), ("draw", 0), ("loss", -1)):
+        p = float((w == val).mean())
+        out[key] = z(p, ref[key], p * (1 - p))
+    out["steps_per_game"] = z(L.mean(), ref["steps"] / m, L.var())
+    for key, col in (("reward_per_game", "return"), ("reward2_per_game", "return2")):
+        r = per_game[col]
+        out[key] = z(r.mean(), ref[key.replace("_per_game", "_sum")] / m, r.var())
+    mu = per_game["obs_sum"].sum(0) / L.sum()
+    resid = per_game["obs_sum"] - L[:, None] * mu[None, :]  # linearised ratio estimator
+    var1 = (resid ** 2).mean(0) / L.mean() ** 2
+    out["obs_mean"] = [z(mu[k], ref["obs_mean"][k], var1[k]) for k in range(18)]
+    return out
