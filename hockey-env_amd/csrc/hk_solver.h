@@ -253,10 +253,12 @@ HK_DEV f2 rel_vel(f2 vA, float wA, f2 vB, float wB, f2 rA, f2 rB) {
 // kSA: body A is static, so vA = wA = +0 at every solve (the callers reset them) and A's updates are dead.
 // The relative velocity then keeps only the operations that can change a bit: u - (+0) == u for every u,
 // but u - (+0)*perp(rA) can turn a -0 of u into +0, so that product stays (loop-invariant, hoisted).
-template <bool kSA = false>
+// kP: the manifold's point count when the caller knows it for every lane running the call (1 or 2), else 0
+// (read per lane): a wave whose lanes all solve one-point contacts skips the block solver's code entirely.
+template <bool kSA = false, int kP = 0>
 HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &wB) {
   const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
-  const int vcount = fs_vcount(s);
+  const int vcount = kP ? kP : fs_vcount(s);
   const f2 normal = f2{s.nx, s.ny}, tangent = f2{1.0f * s.ny, -1.0f * s.nx};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -483,33 +485,38 @@ template <typename SL> struct SlotCap;
 template <int C> struct SlotCap<RegSlots<C>> { static constexpr int value = C; };
 template <> struct SlotCap<HbmSlots> { static constexpr int value = kBigC; };
 
-// One-contact solve (the common case, and the usual owner of a wave's 180-iteration tail): the two bodies'
+// ------------------------------------------------------------------------------------------------
+// Velocity-loop families and the wave's re-dispatch.  A wave runs the cheapest loop that covers the lanes
+// still iterating, and re-picks it every few iterations: most solves exit periodic within 8-16 iterations,
+// and the wave's 180-iteration tail then runs only the code its remaining lanes need (one-contact before
+// two-contact before the general slot loop; one-point rows without the block solver; the static-body-A
+// row).  Every variant computes the same float operations in the same order for the lanes it runs, and a
+// lane's snapshot chain is carried across variants of a family, so the result is bit-identical to 180
+// iterations of the body-file loop.  A family switch restarts the snapshot (the next comparison is skipped).
+// ------------------------------------------------------------------------------------------------
+HK_DEV int chunk_end(int it) {
+  const int e = it + (it < 24 ? 8 : 32);
+  return e < kVelIters ? e : kVelIters;
+}
+static_assert(kVelIters % 4 == 0, "the snapshot period divides the iteration count");
+
+// One-contact family (the common case, and the usual owner of a wave's 180-iteration tail): the two bodies'
 // velocities stay in locals for the whole loop instead of round-tripping through the body file's selects
 // every iteration.  A static body's velocity is re-read as +0 at every iteration, exactly what get_vel
 // returns in the general loop; the snapshot compares the same values the general loop compares.
-template <bool kSA>
-HK_DEV int velocity_iterations_one_t(FSlot &s, Dyn &B) {
-  const int bA = fs_bA(s), bB = fs_bB(s);
-  const bool dynA = !kSA && bA < 3;
-  v2 vA2, vB2;
-  float wA, wB;
-  get_vel_a(B, bA, vA2, wA);
-  get_vel_b(B, bB, vB2, wB);
-  f2 vA = F2(vA2), vB = F2(vB2);
-  uint32_t sn[10];
-#pragma unroll
-  for (int k = 0; k < 10; ++k) sn[k] = 0u;
-  int it = 0;
-  bool active = true;
+// kSA: no running lane has a dynamic body A, so A's velocity row is dropped (fslot_solve_velocity_p).
+template <bool kSA, int kP>
+HK_DEV void vone_chunk(FSlot &s, bool dynA, f2 &vA, float &wA, f2 &vB, float &wB, uint32_t (&sn)[10], int &it,
+                       int stop, int first, bool &active) {
   HK_MARK(vone_begin);
-  for (; it < kVelIters && active; it += 4) {
+  for (; it < stop && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!dynA) {
         vA = f2{0.0f, 0.0f};
         wA = 0.0f;
       }
-      fslot_solve_velocity_p<kSA>(s, vA, wA, vB, wB);
+      fslot_solve_velocity_p<kSA, kP>(s, vA, wA, vB, wB);
     }
     const uint32_t x[10] = {__float_as_uint(vB[0]), __float_as_uint(vB[1]), __float_as_uint(wB),
                             dynA ? __float_as_uint(vA[0]) : 0u, dynA ? __float_as_uint(vA[1]) : 0u,
@@ -521,59 +528,75 @@ HK_DEV int velocity_iterations_one_t(FSlot &s, Dyn &B) {
       diff |= x[k] ^ sn[k];
       sn[k] = x[k];
     }
-    if (it + 3 >= 7 && diff == 0u) active = false;
+    if (it + 3 >= first && diff == 0u) active = false;
   }
   HK_MARK(vone_end);
-  if (dynA) set_vel_a(B, bA, V2(vA), wA);
-  set_vel_b(B, bB, V2(vB), wB);
-  return it;
+  if (it >= kVelIters) active = false;  // 180 iterations done
 }
-// waves whose one-contact solves all have a static body A (every TOI solve, wall contacts) take the
-// static-A row
-HK_DEV int velocity_iterations_one(FSlot &s, Dyn &B) {
-  if (!wave_any(fs_bA(s) < 3)) return velocity_iterations_one_t<true>(s, B);
-  return velocity_iterations_one_t<false>(s, B);
+HK_DEV void vone_family(FSlot &s, Dyn &B, int &it, bool &active, int first) {
+  const bool entered = active;
+  const int bA = fs_bA(s), bB = fs_bB(s), vc = fs_vcount(s);
+  const bool dynA = bA < 3;
+  v2 vA2, vB2;
+  float wA, wB;
+  get_vel_a(B, bA, vA2, wA);
+  get_vel_b(B, bB, vB2, wB);
+  f2 vA = F2(vA2), vB = F2(vB2);
+  uint32_t sn[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) sn[k] = 0u;
+  while (wave_any(active)) {
+    const int stop = chunk_end(it);
+    const bool sa = !wave_any(active && dynA);
+    const bool p1 = !wave_any(active && vc != 1), p2 = !wave_any(active && vc != 2);
+    if (sa) {
+      if (p1) vone_chunk<true, 1>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else if (p2) vone_chunk<true, 2>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else vone_chunk<true, 0>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+    } else {
+      if (p1) vone_chunk<false, 1>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else if (p2) vone_chunk<false, 2>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else vone_chunk<false, 0>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+    }
+  }
+  if (entered) {
+    if (dynA) set_vel_a(B, bA, V2(vA), wA);
+    set_vel_b(B, bB, V2(vB), wB);
+  }
 }
 
-// Two-contact solve (waves whose islands all have at most two contacts; a one-contact lane runs it with
-// contact 1 masked off).  Each contact keeps its two bodies' velocities in locals; after a contact is
-// solved, the other contact's copy of any body it shares (equal body index) is refreshed from it, so every
-// solve reads exactly the velocities the body-file loop reads, at 2 selects per shared-body component
-// instead of the body file's gather and scatter.  A static body A is +0 at every solve, as get_vel_a
-// returns it.  The snapshot covers every island body (each appears in some contact) and both contacts'
-// impulses: the set the general loop compares, some bodies twice.
+// Two-contact family (islands of at most two contacts; a one-contact lane runs it with contact 1 masked
+// off).  Each contact keeps its two bodies' velocities in locals; after a contact is solved, the other
+// contact's copy of any body it shares (equal body index) is refreshed from it, so every solve reads exactly
+// the velocities the body-file loop reads, at 2 selects per shared-body component instead of the body file's
+// gather and scatter.  A static body A is +0 at every solve, as get_vel_a returns it.  The snapshot covers
+// every island body (each appears in some contact) and both contacts' impulses: the set the general loop
+// compares, some bodies twice.
 HK_DEV f2 sel2(bool c, f2 a, f2 b) { return f2{c ? a[0] : b[0], c ? a[1] : b[1]}; }
-HK_DEV int velocity_iterations_two(FSlot &s0, FSlot &s1, Dyn &B, int nc) {
-  if (nc == 0) return 0;
-  const bool two = nc == 2;
-  const int a0 = fs_bA(s0), b0 = fs_bB(s0);
-  const int a1 = two ? fs_bA(s1) : 15, b1 = two ? fs_bB(s1) : 15;  // 15: matches no body
-  const bool dA0 = a0 < 3, dA1 = a1 < 3;
-  const bool a1a0 = a1 == a0, a1b0 = a1 == b0, b1a0 = b1 == a0, b1b0 = b1 == b0;
-  v2 t;
+struct TwoState {
+  f2 vA0, vB0, vA1, vB1;
   float wA0, wB0, wA1, wB1;
-  get_vel_a(B, a0, t, wA0);
-  f2 vA0 = F2(t);
-  get_vel_b(B, b0, t, wB0);
-  f2 vB0 = F2(t);
-  get_vel_a(B, a1, t, wA1);
-  f2 vA1 = F2(t);
-  get_vel_b(B, b1, t, wB1);
-  f2 vB1 = F2(t);
+  uint32_t sn[20];
+};
+template <int kP0, int kP1>
+HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool dA0, bool dA1, bool a1a0, bool a1b0,
+                       bool b1a0, bool b1b0, int &it, int stop, int first, bool &active) {
+  // the state lives in this function's own locals for the loop (selects between fields of a by-reference
+  // struct turn into pointer selects, which keep the struct in scratch memory)
+  f2 vA0 = t.vA0, vB0 = t.vB0, vA1 = t.vA1, vB1 = t.vB1;
+  float wA0 = t.wA0, wB0 = t.wB0, wA1 = t.wA1, wB1 = t.wB1;
   uint32_t sn[20];
 #pragma unroll
-  for (int k = 0; k < 20; ++k) sn[k] = 0u;
-  int it = 0;
-  bool active = true;
+  for (int k = 0; k < 20; ++k) sn[k] = t.sn[k];
   HK_MARK(vtwo_begin);
-  for (; it < kVelIters && active; it += 4) {
+  for (; it < stop && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!dA0) {
         vA0 = f2{0.0f, 0.0f};
         wA0 = 0.0f;
       }
-      fslot_solve_velocity_p(s0, vA0, wA0, vB0, wB0);
+      fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
       vA1 = sel2(a1a0, vA0, sel2(a1b0, vB0, vA1));
       wA1 = a1a0 ? wA0 : (a1b0 ? wB0 : wA1);
       vB1 = sel2(b1a0, vA0, sel2(b1b0, vB0, vB1));
@@ -583,7 +606,7 @@ HK_DEV int velocity_iterations_two(FSlot &s0, FSlot &s1, Dyn &B, int nc) {
           vA1 = f2{0.0f, 0.0f};
           wA1 = 0.0f;
         }
-        fslot_solve_velocity_p(s1, vA1, wA1, vB1, wB1);
+        fslot_solve_velocity_p<false, kP1>(s1, vA1, wA1, vB1, wB1);
         vA0 = sel2(a1a0, vA1, sel2(b1a0, vB1, vA0));
         wA0 = a1a0 ? wA1 : (b1a0 ? wB1 : wA0);
         vB0 = sel2(a1b0, vA1, sel2(b1b0, vB1, vB0));
@@ -605,42 +628,68 @@ HK_DEV int velocity_iterations_two(FSlot &s0, FSlot &s1, Dyn &B, int nc) {
       diff |= x[k] ^ sn[k];
       sn[k] = x[k];
     }
-    if (it + 3 >= 7 && diff == 0u) active = false;
+    if (it + 3 >= first && diff == 0u) active = false;
   }
   HK_MARK(vtwo_end);
-  if (dA0) set_vel_a(B, a0, V2(vA0), wA0);
-  set_vel_b(B, b0, V2(vB0), wB0);
-  if (two) {
-    if (dA1) set_vel_a(B, a1, V2(vA1), wA1);
-    set_vel_b(B, b1, V2(vB1), wB1);
-  }
-  return it;
+  if (it >= kVelIters) active = false;
+  t.vA0 = vA0; t.vB0 = vB0; t.vA1 = vA1; t.vB1 = vB1;
+  t.wA0 = wA0; t.wB0 = wB0; t.wA1 = wA1; t.wB1 = wB1;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) t.sn[k] = sn[k];
 }
-
-// 180 velocity iterations over nc slots, with the exact periodic early exit
-template <typename SL>
-HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
-  if constexpr (SL::kRegister) {
-    // the one-contact loop only when no active lane of the wave solves a larger island, the two-contact
-    // loop (which also serves the wave's one-contact lanes) only when none solves more than two: a wave
-    // never runs two of these loops one after the other (which would lengthen the slowest waves)
-    if (!wave_any(nc > 1)) {
-      if (nc == 1) return velocity_iterations_one(S.s[0], B);
-    } else if (!wave_any(nc > 2)) {
-      return velocity_iterations_two(S.s[0], S.s[1], B, nc);
+// runs until every lane is done or no running lane has two contacts (then the one-contact family takes over)
+HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, int nc, int &it, bool &active, int first) {
+  const bool entered = active;
+  const bool two = nc == 2;
+  const int a0 = fs_bA(s0), b0 = fs_bB(s0);
+  const int a1 = two ? fs_bA(s1) : 15, b1 = two ? fs_bB(s1) : 15;  // 15: matches no body
+  const bool dA0 = a0 < 3, dA1 = a1 < 3;
+  const bool a1a0 = a1 == a0, a1b0 = a1 == b0, b1a0 = b1 == a0, b1b0 = b1 == b0;
+  const int vc0 = fs_vcount(s0), vc1 = two ? fs_vcount(s1) : 1;
+  TwoState t;
+  v2 q;
+  get_vel_a(B, a0, q, t.wA0);
+  t.vA0 = F2(q);
+  get_vel_b(B, b0, q, t.wB0);
+  t.vB0 = F2(q);
+  get_vel_a(B, a1, q, t.wA1);
+  t.vA1 = F2(q);
+  get_vel_b(B, b1, q, t.wB1);
+  t.vB1 = F2(q);
+#pragma unroll
+  for (int k = 0; k < 20; ++k) t.sn[k] = 0u;
+  while (wave_any(active) && wave_any(active && two)) {
+    const int stop = chunk_end(it);
+    if (!wave_any(active && (vc0 != 1 || vc1 != 1)))
+      vtwo_chunk<1, 1>(s0, s1, t, two, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active);
+    else
+      vtwo_chunk<0, 0>(s0, s1, t, two, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active);
+  }
+  if (entered) {
+    if (dA0) set_vel_a(B, a0, V2(t.vA0), t.wA0);
+    set_vel_b(B, b0, V2(t.vB0), t.wB0);
+    if (two) {
+      if (dA1) set_vel_a(B, a1, V2(t.vA1), t.wA1);
+      set_vel_b(B, b1, V2(t.vB1), t.wB1);
     }
   }
+}
+
+// General family: the slot loop over the body file (any island size, register or HBM slots).  With
+// `leave`, it returns after a chunk once no running lane has more than two contacts.
+template <typename SL>
+HK_DEV void vgen_family(SL &S, Dyn &B, int nc, int &it, bool &active, int first, bool leave) {
   uint32_t sb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) sb[k] = 0u;
-  bool active = nc > 0;
-  int it = 0;
-  static_assert(kVelIters % 4 == 0, "the snapshot period divides the iteration count");
-  HK_MARK(vit_begin);
-  for (; it < kVelIters && active; it += 4) {  // 4 iterations per trip: the snapshot period
+  S.each(nc, [&](FSlot &s, int) { s.sn[0] = s.sn[1] = s.sn[2] = s.sn[3] = 0u; });
+  while (wave_any(active)) {
+    if (leave && !wave_any(active && nc > 2)) return;
+    const int stop = chunk_end(it);
+    HK_MARK(vit_begin);
+    for (; it < stop && active; it += 4) {  // 4 iterations per trip: the snapshot period
 #pragma unroll
-    for (int u = 0; u < 4; ++u) S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
-    {
+      for (int u = 0; u < 4; ++u) S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
       uint32_t diff = 0u;
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
@@ -659,10 +708,31 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
         s.sn[2] = x2;
         s.sn[3] = x3;
       });
-      if (it + 3 >= 7 && diff == 0u) active = false;
+      if (it + 3 >= first && diff == 0u) active = false;
     }
+    HK_MARK(vit_end);
+    if (it >= kVelIters) active = false;
   }
-  HK_MARK(vit_end);
+}
+
+// 180 velocity iterations over nc slots, with the exact periodic early exit (register slots: the wave walks
+// the families general -> two -> one as its running lanes allow; HBM slots: the general loop)
+template <typename SL>
+HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
+  int it = 0;
+  bool active = nc > 0;
+  int first = 7;  // the first comparison against a snapshot taken by this loop (it + 3 == 7)
+  if constexpr (SL::kRegister) {
+    static_assert(SlotCap<SL>::value >= 2, "the one- and two-contact families use slots 0 and 1");
+    while (wave_any(active)) {
+      if (wave_any(active && nc > 2)) vgen_family(S, B, nc, it, active, first, true);
+      else if (wave_any(active && nc > 1)) vtwo_family(S.s[0], S.s[1], B, nc, it, active, first);
+      else vone_family(S.s[0], B, it, active, first);
+      first = it + 7;  // the next family starts a fresh snapshot
+    }
+  } else {
+    vgen_family(S, B, nc, it, active, first, false);
+  }
   return it;
 }
 
