@@ -94,7 +94,7 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NIF * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
   const size_t nw = (size_t)hk::workspace_words_per_arena() * n;
   if ((e = hipMalloc(&c->s.f, nf * 4)) != hipSuccess || (e = hipMalloc(&c->s.i, ni * 4)) != hipSuccess ||
-      (e = hipMalloc(&c->s.man, nm * 4)) != hipSuccess || (e = hipMalloc(&c->s.phase, 2 * n * 8)) != hipSuccess ||
+      (e = hipMalloc(&c->s.man, nm * 4)) != hipSuccess || (e = hipMalloc(&c->s.phase, 3 * n * 8)) != hipSuccess ||
       (e = hipMalloc(&c->s.ws, nw * 4)) != hipSuccess || (e = hipMalloc(&c->s.counters, HK_NUM_COUNTERS * 8)) != hipSuccess) {
     hk_destroy(c);
     return hipfail(e, "hk_create: hipMalloc");
@@ -170,6 +170,7 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
   s.debug = io->debug;
   s.final_obs = io->final_obs;
   s.flags = io->flags;
+  s.policy2 = io->policy2;
   DeviceGuard g(c->device);
   hipError_t e = hk::launch_step(c->s, c->cfg, s, nsteps, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, who);

@@ -24,7 +24,8 @@ struct DevState {
   int32_t *i;
   float *man;  // manifold records [NSOLID][N][NMF] (64 B per record, hk_arena.h ManRec)
   float *ws;  // large-island slot workspace [kBigC][kSlotWords][N] (hk_solver.h HbmSlots)
-  double *phase;
+  double *phase;  // BasicOpponent phases [3][N]: player 1, player 2 (its policy / the strong bot under a
+                  // per-arena override), player 2's weak bot under an override (hk_step_io.policy2)
   unsigned long long *counters;
   int64_t n;
 };
@@ -44,6 +45,7 @@ struct StepIO {
   uint8_t *done;
   float *info, *info2, *actions_out, *debug, *final_obs;
   int flags;
+  const uint8_t *policy2;  // per-arena player-2 policy override (hk_step_io.policy2) or nullptr
 };
 
 hipError_t launch_init(const DevState &s, const KCfg &cfg, hipStream_t st);

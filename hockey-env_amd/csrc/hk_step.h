@@ -257,7 +257,11 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   // ---- actions: external / Philox random / fused BasicOpponent ----
   float a8[8];
   for (int p = 0; p < 2; ++p) {
-    const int pol = cfg.policy[p];
+    int pol = cfg.policy[p], row = p;  // row: the acting BasicOpponent's phase (DevState::phase)
+    if (p == 1 && io.policy2) {
+      pol = io.policy2[a];
+      row = pol == 2 ? 2 : 1;
+    }
     if (pol == 0) {
       for (int k = 0; k < 4; ++k) a8[4 * p + k] = io.actions ? io.actions[a * 8 + 4 * p + k] : 0.0f;
     } else if (pol == 1) {
@@ -277,9 +281,9 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
         U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), stepc, RNG_PHASE + 0x10 * p);
         inc = 0.0 + (0.2 - 0.0) * u01d(r.x, r.y);
       }
-      double ph = s.phase[p * s.n + a];
+      double ph = s.phase[row * s.n + a];
       basic_opponent(pol == 2, w.keep_mode, ph, inc, o, &a8[4 * p]);
-      s.phase[p * s.n + a] = ph;
+      s.phase[row * s.n + a] = ph;
     }
   }
   if (io.actions_out)
@@ -453,7 +457,7 @@ HK_DEV void init_lane(const DevState &s, const KCfg &cfg, int64_t a) {
   // HockeyEnv.__init__ sets one_starts = True and resets with one_starting=True (hockey_env.py:117,155);
   // hk_create's first reset toggles this 0 -> 1.
   I(s, I_ONE, a) = 0;
-  for (int p = 0; p < 2; ++p) {
+  for (int p = 0; p < 3; ++p) {  // row 2: player 2's weak bot under a per-arena override
     const int64_t ga = cfg.arena_offset + a;
     U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), 0, RNG_PHASE0 + 0x10 * p);
     s.phase[p * s.n + a] = 0.0 + (kPiD - 0.0) * u01d(r.x, r.y);  // BasicOpponent.__init__ U(0, pi)

@@ -35,7 +35,7 @@ class StepIO(ctypes.Structure):
                 ("obs2", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("reward2", ctypes.c_void_p),
                 ("done", ctypes.c_void_p), ("info", ctypes.c_void_p), ("info2", ctypes.c_void_p),
                 ("actions_out", ctypes.c_void_p), ("debug", ctypes.c_void_p), ("final_obs", ctypes.c_void_p),
-                ("flags", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("policy2", ctypes.c_void_p)]
 
 
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",

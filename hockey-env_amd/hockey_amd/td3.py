@@ -15,10 +15,15 @@ Mirrors the reference's learner and collection semantics on device tensors end t
   breaking on done (the env's done is sticky, so post-goal steps repeat the terminal reward) and every
   transition is stored with ``done``; ``train_iters`` updates follow each episode.
 
+* opponents: rl/training/opponent_manager.py + self_play.py + curricula.py (``hockey_amd.opponents``) --
+  player 2 of every arena is re-drawn every step (self-play snapshot / strong bot / weak bot) from the
+  curriculum row of the training progress; the bots run fused in the kernel (``hk_step_io.policy2``), the
+  step's self-play snapshot as one batched actor forward; the pool snapshots the actor every
+  ``self_play_interval`` episodes.
+
 Batched differences (by design): N episodes run side by side (one arena each) and their transitions enter
-one device replay ring; updates per round scale with N through ``updates_per_round``; player 2 is the
-fused BasicOpponent, weak on the first ``weak_fraction`` of the arenas and strong on the rest (two step
-contexts), instead of the reference's adaptive opponent manager / self-play pool.
+one device replay ring; updates per round scale with N through ``updates_per_round``; see
+``hockey_amd.opponents`` for the opponent draws.
 """
 from dataclasses import dataclass
 
@@ -180,50 +185,51 @@ class TD3:
                 "target_policy": self.target_actor.state_dict(), "target_critic": self.target_critic.state_dict()}
 
 
-def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, weak_fraction=0.5, updates_per_round=None,
-          mode=Mode.NORMAL, log=None):
+def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_per_round=None, mode=Mode.NORMAL,
+          curriculum="stage3", use_self_play=True, self_play_interval=100, pool_size=40, log=None):
     """Batched TD3 training: each round runs ``max_steps`` steps of ``n_arenas`` parallel episodes (no break on
     done), stores every transition, then performs ``updates_per_round`` learner updates (default: the
-    reference's ``train_iters`` per episode, scaled by n_arenas / 64).  Returns (agent, stats)."""
+    reference's ``train_iters`` per episode, scaled by n_arenas / 64).  Player 2 follows the curriculum's
+    opponent mix (``hockey_amd.opponents.OpponentMix``), re-drawn per arena and step.  Returns (agent, stats)."""
+    from .opponents import OpponentMix
     from .vec_env import VecHockeyEnv
 
     cfg = cfg or TD3Config()
     agent = TD3(cfg, device, seed)
-    n_weak = int(round(n_arenas * weak_fraction))
-    groups = [(n, pol) for n, pol in ((n_weak, "weak"), (n_arenas - n_weak, "strong")) if n > 0]
-    envs = [VecHockeyEnv(n, mode=mode, device=device, policies=("external", pol), auto_reset=False,
-                         seed=seed + 7919 * k, arena_offset=sum(g[0] for g in groups[:k]))
-            for k, (n, pol) in enumerate(groups)]
+    env = VecHockeyEnv(n_arenas, mode=mode, device=device, policies=("external", "external"), auto_reset=False,
+                       seed=seed)
+    mix = OpponentMix(n_arenas, curriculum, use_self_play, self_play_interval, pool_size, device, seed)
     ring = ReplayRing(min(cfg.buffer_size, n_arenas * cfg.max_steps * 4), device=device)
     updates = updates_per_round or max(1, cfg.train_iters * n_arenas // 64)
     planned = rounds * cfg.max_steps * n_arenas
-    agent_steps, stats = 0, {"env_steps": 0, "updates": 0, "critic_loss": [], "actor_loss": [], "mean_reward": []}
+    act8 = torch.zeros((n_arenas, 8), device=device)
+    agent_steps = 0
+    stats = {"env_steps": 0, "updates": 0, "critic_loss": [], "actor_loss": [], "mean_reward": [], "opponents": [],
+             "pool_size": []}
     for rnd in range(rounds):
-        obs = []
-        for k, env in enumerate(envs):  # episode i of this round resets with seed + round * n_arenas + i
-            p, _, _ = reset_params(env.n, seed + rnd * n_arenas + sum(g[0] for g in groups[:k]), mode)
-            env.reset_params(p)
-            obs.append(env.observe()[0].clone())
+        mix.update_schedule(rnd / rounds)
+        # episode i of this round resets with seed + round * n_arenas + i (the reference: seed + episode)
+        p, _, _ = reset_params(n_arenas, seed + rnd * n_arenas, mode)
+        env.reset_params(p)
+        obs, obs2 = (t.clone() for t in env.observe())
         ep_reward = torch.zeros(n_arenas, device=device)
         for _ in range(cfg.max_steps):
-            o = torch.cat(obs)
-            a = agent.act(o, agent_steps, planned)
+            a = agent.act(obs, agent_steps, planned)
             agent_steps += n_arenas
-            nxt, rew, dn, lo = [], [], [], 0
-            for k, env in enumerate(envs):
-                act = torch.zeros((env.n, 8), device=device)
-                act[:, :4] = a[lo:lo + env.n]
-                res = env.step(act)
-                nxt.append(res.obs.clone())
-                rew.append(res.reward.clone())
-                dn.append(res.done.clone())
-                lo += env.n
-            o2, r, d = torch.cat(nxt), torch.cat(rew), torch.cat(dn)
-            ring.push(o, a, r, o2, d)
+            policy2, a2, _ = mix.select(obs2)
+            act8[:, :4] = a
+            if a2 is not None:
+                act8[:, 4:] = a2
+            res = env.step(act8, with_agent_two=True, policy2=policy2)
+            o2, r, d = res.obs.clone(), res.reward.clone(), res.done.clone()
+            ring.push(obs, a, r, o2, d)
+            mix.register_outcomes(d, r)
             ep_reward += r
-            obs = nxt
+            obs, obs2 = o2, res.obs2.clone()
         stats["env_steps"] += cfg.max_steps * n_arenas
         stats["mean_reward"].append(float(ep_reward.mean().item()))
+        stats["opponents"].append(mix.end_round(agent.actor, episodes=n_arenas))
+        stats["pool_size"].append(len(mix.pool) if mix.pool is not None else 0)
         if agent_steps > cfg.batch_size:
             for _ in range(updates):
                 al, cl = agent.update(*ring.sample(cfg.batch_size))
@@ -233,8 +239,8 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, weak_frac
                     stats["actor_loss"].append(al)
         if log:
             log(rnd, stats)
-    for env in envs:
-        env.close()
+    env.close()
     stats["critic_loss"] = [float(x) for x in stats["critic_loss"]]
     stats["actor_loss"] = [float(x) for x in stats["actor_loss"]]
+    stats["replay_size"] = len(ring)
     return agent, stats

@@ -146,13 +146,17 @@ class VecHockeyEnv:
 
     # ------------------------------------------------------------------ step
     def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=None, skip_physics=False,
-             record_actions=False, final_obs=False):
+             record_actions=False, final_obs=False, policy2=None):
         """HockeyEnv.step for every arena.  actions: [N,8] float (clipped in-kernel), may be None when no
         player is external.  Returns a StepResult of device tensors (views of persistent buffers).
 
         With auto_reset, an arena that is done after this step is reset at its end: done / reward / info are
         the terminal step's, obs / obs2 the new episode's first state, and ``final_obs`` (when requested) the
-        terminal observation (== obs for arenas that did not reset)."""
+        terminal observation (== obs for arenas that did not reset).
+
+        policy2 ([N] uint8 / policy ids, optional): player 2's policy of each arena for this step, overriding
+        the context's (rl/training/opponent_manager.py draws the opponent per step); 'external' arenas read
+        actions[:, 4:8]."""
         a = None
         if actions is not None:
             a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
@@ -180,6 +184,12 @@ class VecHockeyEnv:
         if final_obs:
             io.final_obs = self.final_obs_buf.data_ptr()
         io.flags = N.STEP_SKIP_PHYSICS if skip_physics else 0
+        p2 = None
+        if policy2 is not None:
+            p2 = torch.as_tensor(policy2, dtype=torch.uint8, device=self.device).contiguous()
+            if p2.shape != (self.n,):
+                raise ValueError(f"policy2 must have shape ({self.n},), got {tuple(p2.shape)}")
+            io.policy2 = p2.data_ptr()
         N.check(self.L.hk_step(self._ctx, ctypes.byref(io), self._stream()), "hk_step")
         return StepResult(obs=self.obs_buf, reward=self.reward_buf, done=self.done_buf, info=self.info_buf,
                           obs2=self.obs2_buf if with_agent_two else None,

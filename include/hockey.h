@@ -103,6 +103,11 @@ typedef struct hk_step_io {
   float *final_obs;       /* [N,18] f32 observation after the step's physics (or NULL): the terminal
                              observation of arenas that auto-reset in this step, == obs for the others */
   int32_t flags;          /* HK_STEP_* */
+  const uint8_t *policy2; /* [N] u8 per-arena player-2 policy (HK_POLICY_*) for this step, overriding the
+                             context's, or NULL: rl/training/opponent_manager.py:62-91 draws player 2's
+                             opponent (self-play / strong / weak bot) per step.  EXTERNAL reads actions[:,4:8].
+                             Under an override the strong bot keeps phase row 1 and the weak bot its own row 2
+                             (the reference's OpponentManager holds one BasicOpponent of each kind) */
 } hk_step_io;
 
 const char *hk_last_error(void);

@@ -58,7 +58,7 @@ def lib():
         L.hkov_destroy.argtypes = [vp]
         L.hkov_reset.argtypes = [vp, vp, vp, vp, vp]
         L.hkov_set_policy.argtypes = [vp, ctypes.c_int, ctypes.c_int]
-        L.hkov_step.argtypes = [vp] * 12
+        L.hkov_step.argtypes = [vp] * 13
         L.hkov_get_state.argtypes = [vp, vp, vp]
         L.hkov_set_state.argtypes = [vp, vp, vp, vp]
         L.hkov_observe.argtypes = [vp, vp, vp]
@@ -200,8 +200,9 @@ class OracleVec:
     def set_policy(self, player, policy):
         self._L.hkov_set_policy(self._v, int(player), POLICY[policy] if isinstance(policy, str) else int(policy))
 
-    def step(self, actions=None, opp_inc=None, with_agent_two=False, final_obs=False):
+    def step(self, actions=None, opp_inc=None, with_agent_two=False, final_obs=False, policy2=None):
         n = self.n
+        p2 = None if policy2 is None else np.ascontiguousarray(policy2, np.uint8).reshape(n)
         a = None if actions is None else np.ascontiguousarray(actions, np.float32).reshape(n, 8)
         inc = None if opp_inc is None else np.ascontiguousarray(opp_inc, np.float64).reshape(n, 2)
         out = {"obs": np.zeros((n, 18), np.float32), "reward": np.zeros(n, np.float32),
@@ -214,7 +215,8 @@ class OracleVec:
             out["final_obs"] = np.zeros((n, 18), np.float32)
         g = out.get
         self._L.hkov_step(self._v, _p(a), _p(inc), _p(g("obs")), _p(g("obs2")), _p(g("reward")), _p(g("reward2")),
-                          _p(g("done")), _p(g("info")), _p(g("info2")), _p(g("actions")), _p(g("final_obs")))
+                          _p(g("done")), _p(g("info")), _p(g("info2")), _p(g("actions")), _p(g("final_obs")),
+                          _p(p2))
         return out
 
     def get_state(self):

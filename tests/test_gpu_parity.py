@@ -328,6 +328,29 @@ def test_random_policies_lockstep_vs_oracle(oracle):
     assert "field" not in out, out
 
 
+def test_per_step_opponent_mix_lockstep_vs_oracle(oracle):
+    """C5's opponent mix (rl/training/opponent_manager.py:62-91): player 2's policy drawn per arena and step
+    from {external (self-play actions), weak bot, strong bot} through hk_step_io.policy2, each bot with its
+    own phase -- bit-exact against the oracle over episodes with auto-reset."""
+    n, steps = 256, 400
+    env = _vec(n, mode=0, policies=("external", "external"), auto_reset=True, seed=31)
+    ov = oracle.OracleVec(n, mode=0, policies=("external", "external"), auto_reset=True, seed=31)
+    rng = np.random.default_rng(31)
+    for t in range(steps):
+        a = rng.uniform(-1, 1, (n, 8)).astype(np.float32)
+        p2 = rng.choice(np.array([0, 2, 3], np.uint8), n)
+        got = _res_np(env.step(a, with_agent_two=True, record_actions=True, final_obs=True,
+                               policy2=torch.as_tensor(p2, device="cuda:0")))
+        want = ov.step(a, with_agent_two=True, final_obs=True, policy2=p2)
+        bad = first_mismatch(t, got, want)
+        assert bad is None, bad
+    st, aux = env.get_state()
+    ost, oaux = ov.get_state()
+    assert np.array_equal(st.cpu().numpy(), ost) and np.array_equal(aux.cpu().numpy(), oaux)
+    assert env.counters()[N.CNT_EPISODES] > 0
+    env.close()
+
+
 def test_large_island_path_on_gpu_vs_oracle(oracle):
     """HK_DIAG_LARGE_ISLANDS: every island / TOI mini-island solved on the HBM slot file (the path islands
     beyond the register slots take in production) -- bit-exact on gfx950 too."""

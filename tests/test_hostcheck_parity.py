@@ -94,16 +94,18 @@ def test_fused_opponents_autoreset_run(oracle):
 from vec_lockstep import first_mismatch  # noqa: E402
 
 
-def _vec_lockstep(oracle, n, steps, mode, policies, seed, external=False, offset=0):
+def _vec_lockstep(oracle, n, steps, mode, policies, seed, external=False, offset=0, mix=False):
     """The kernel source (host build) vs the oracle's batched context on the hk_step contract: fused
-    policies with Philox increments (opp_inc NULL), device auto-reset with episode counters."""
+    policies with Philox increments (opp_inc NULL), device auto-reset with episode counters.  mix: player 2's
+    policy is drawn per arena and step from {external, weak, strong} (hk_step_io.policy2)."""
     env = HostVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
     ov = oracle.OracleVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
     rng = np.random.default_rng(seed)
     for t in range(steps):
         acts = rng.uniform(-1.2, 1.2, (n, 8)).astype(np.float32) if external else None
-        got = vars(env.step(acts, with_agent_two=True, record_actions=True, final_obs=True))
-        want = ov.step(acts, with_agent_two=True, final_obs=True)
+        p2 = rng.choice(np.array([0, 2, 3], np.uint8), n) if mix else None
+        got = vars(env.step(acts, with_agent_two=True, record_actions=True, final_obs=True, policy2=p2))
+        want = ov.step(acts, with_agent_two=True, final_obs=True, policy2=p2)
         bad = first_mismatch(t, got, want)
         if bad:
             return bad
@@ -128,4 +130,13 @@ def test_random_and_external_policies_vs_oracle_vec(oracle):
     out = _vec_lockstep(oracle, 48, 300, 0, ("random", "weak"), seed=21, offset=1000)
     assert "field" not in out, out
     out = _vec_lockstep(oracle, 48, 300, 2, ("external", "strong"), seed=22, external=True)
+    assert "field" not in out, out
+
+
+def test_per_step_opponent_mix_vs_oracle_vec(oracle):
+    """Player 2's opponent drawn per arena and step (hk_step_io.policy2, rl/training/opponent_manager.py:62-91):
+    external (self-play actions), weak bot and strong bot, each bot with its own phase."""
+    out = _vec_lockstep(oracle, 48, 300, 0, ("external", "external"), seed=23, external=True, mix=True)
+    assert "field" not in out, out
+    out = _vec_lockstep(oracle, 32, 200, 1, ("strong", "weak"), seed=24, external=True, mix=True)
     assert "field" not in out, out

@@ -1,6 +1,7 @@
 """§8 row f3: the GPU-resident TD3 (hockey_amd/td3.py).  CPU tests pin the learner arithmetic against the
 reference formulas (rl/td3/learner.py:55-218, rl/utils/torch_utils.py:12-24); the GPU test runs the batched
 collection + update loop over real arenas."""
+import numpy as np
 import pytest
 import torch
 
@@ -68,3 +69,28 @@ def test_batched_training_loop_runs():
     assert all(torch.isfinite(torch.tensor(st["critic_loss"]))) and len(st["actor_loss"]) == 30
     x = torch.zeros(4, 18, device="cuda:0")
     assert torch.isfinite(agent.actor(x)).all()
+
+
+@pytest.mark.gpu
+def test_c5_training_loop_65536_arenas_with_opponent_mix():
+    """BASELINE C5: the TD3 loop fed by 65 536 GPU arenas, player 2 re-drawn per arena and step between the
+    strong bot, the weak bot and a self-play snapshot (rl/training/opponent_manager.py:62-91); the pool
+    snapshots the actor every 65 536 episodes, i.e. after every round here."""
+    from hockey_amd.td3 import train
+
+    n, rounds, steps = 65536, 3, 40
+    cfg = TD3Config(max_steps=steps, start_steps=0, batch_size=256)
+    agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, updates_per_round=10, seed=5,
+                      curriculum=[(1.0, 0.35, 0.35, 0.30)], self_play_interval=n, pool_size=2)
+    assert st["env_steps"] == rounds * steps * n
+    assert st["replay_size"] == min(cfg.buffer_size, n * steps * 4)
+    assert st["updates"] == rounds * 10 and len(st["actor_loss"]) == rounds * 5
+    assert all(np.isfinite(st["critic_loss"])) and all(np.isfinite(st["actor_loss"]))
+    assert st["pool_size"] == [1, 2, 2]  # one snapshot per round, capped at pool_size
+    first, *later = st["opponents"]
+    assert first["self_play"] == 0 and first["strong"] + first["weak"] == steps * n  # empty pool: bots only
+    for o in later:
+        assert sum(o.values()) == steps * n
+        assert abs(o["self_play"] / (steps * n) - 0.30) < 0.01
+        assert abs(o["strong"] / (steps * n) - 0.70 * 0.35) < 0.01
+    assert torch.isfinite(agent.actor(torch.zeros(4, 18, device="cuda:0"))).all()
