@@ -53,6 +53,12 @@ def _args():
     ap.add_argument("--cpu-preroll", type=int, default=260, help="CPU baseline: untimed steps first (> 251)")
     ap.add_argument("--cpu-steps", type=int, default=150,
                     help="CPU baseline sample: timed steps (65536 x (260 + 150) is ~15 s on 16 host cores)")
+    ap.add_argument("--facade-steps", type=int, default=2000,
+                    help="also time the single-env gym facade (Hockey-One-v0) this many steps (0 = skip); "
+                         "reported under 'facade_single_env' beside cpu_baseline.single_env")
+    ap.add_argument("--c5-steps", type=int, default=50,
+                    help="also time one C5 TD3 collection round (65 536 arenas, opponent mix) of this many steps "
+                         "(0 = skip); reported under 'c5_collect'")
     ap.add_argument("--streams", type=int, default=2,
                     help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
                          "reported under 'streams'")
@@ -229,6 +235,60 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
             "unit": "env-steps/s", "ms_per_step": elapsed / args.steps * 1e3}
 
 
+def time_facade(steps, dev):
+    """The reference's deployment shape on the GPU: ONE env behind the gym facade (hockey_amd.make
+    ("Hockey-One-v0"): one hk_step launch per env.step plus the host round trip), random agent actions."""
+    import numpy as np
+    import torch
+
+    from hockey_amd import make
+
+    env = make("Hockey-One-v0", device=dev)
+    env.reset(seed=0)
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (steps, 4)).astype(np.float32)
+    for k in range(20):
+        _, _, d, _, _ = env.step(acts[k])
+    env.reset(seed=1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eps = 0
+    for k in range(steps):
+        _, _, d, _, _ = env.step(acts[k])
+        if d:
+            eps += 1
+            env.reset(seed=2 + eps)
+    sec = time.perf_counter() - t0
+    env.close()
+    return {"value": steps / sec, "unit": "env-steps/s", "steps": steps, "episodes": eps,
+            "sample": "1 env, Hockey-One-v0 facade (strong BasicOpponent fused), U(-1,1) agent actions, "
+                      "reset(seed) on done: per step one hk_step launch + obs/reward/done/info copies to the host"}
+
+
+def time_c5(n, steps, dev):
+    """BASELINE C5: one round of the batched TD3 loop (hockey_amd.td3.train): actor forward, per-arena per-step
+    opponent mix (strong / weak bot fused in the kernel, self-play snapshot), hk_step, replay push; the
+    round's single learner update is excluded by timing a warm round against a round of the same shape."""
+    import torch
+
+    from hockey_amd.td3 import TD3Config, train
+
+    cfg = TD3Config(max_steps=steps, start_steps=0)
+    table = [(1.0, 0.35, 0.35, 0.30)]  # stage-3's last curriculum row (self-play active from round 2)
+    train(n_arenas=n, rounds=2, cfg=TD3Config(max_steps=5, start_steps=0), device=dev, updates_per_round=1,
+          curriculum=table, self_play_interval=n)  # warm-up (kernels, allocator)
+    torch.cuda.synchronize()
+    marks = []
+    agent, st = train(n_arenas=n, rounds=2, cfg=cfg, device=dev, updates_per_round=1, curriculum=table,
+                      self_play_interval=n,
+                      log=lambda r, s: (torch.cuda.synchronize(), marks.append(time.perf_counter())))
+    sec = marks[1] - marks[0]  # round 2: the snapshot pool is populated, so the mix includes self-play
+    return {"value": n * steps / sec, "unit": "env-steps/s", "arenas": n, "steps": steps,
+            "opponents": st["opponents"][1],
+            "sample": f"round 2 of hockey_amd.td3.train on {n} arenas x {steps} steps: actor + noise, opponent "
+                      "mix (strong / weak bot / self-play snapshot), hk_step, replay push, 1 learner update"}
+
+
 def main():
     args = _args()
     import torch
@@ -338,6 +398,10 @@ def main():
             line["rollout"] = rollout
         if streams is not None:
             line["streams"] = streams
+        if world == 1 and args.facade_steps > 0:
+            line["facade_single_env"] = time_facade(args.facade_steps, dev)
+        if world == 1 and args.c5_steps > 0:
+            line["c5_collect"] = time_c5(n, args.c5_steps, dev)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_preroll, args.cpu_steps,
                                                 args.seed)
