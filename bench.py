@@ -398,10 +398,17 @@ def main():
             line["rollout"] = rollout
         if streams is not None:
             line["streams"] = streams
+        # side legs: reported beside the headline, never allowed to take the bench line down with them
         if world == 1 and args.facade_steps > 0:
-            line["facade_single_env"] = time_facade(args.facade_steps, dev)
+            try:
+                line["facade_single_env"] = time_facade(args.facade_steps, dev)
+            except Exception as e:  # noqa: BLE001
+                line["facade_single_env"] = {"error": repr(e)[:300]}
         if world == 1 and args.c5_steps > 0:
-            line["c5_collect"] = time_c5(n, args.c5_steps, dev)
+            try:
+                line["c5_collect"] = time_c5(n, args.c5_steps, dev)
+            except Exception as e:  # noqa: BLE001
+                line["c5_collect"] = {"error": repr(e)[:300]}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_preroll, args.cpu_steps,
                                                 args.seed)
