@@ -276,17 +276,17 @@ def time_c5(n, steps, dev):
     cfg = TD3Config(max_steps=steps, start_steps=0)
     table = [(1.0, 0.35, 0.35, 0.30)]  # stage-3's last curriculum row (self-play active from round 2)
     train(n_arenas=n, rounds=2, cfg=TD3Config(max_steps=5, start_steps=0), device=dev, updates_per_round=1,
-          curriculum=table, self_play_interval=n)  # warm-up (kernels, allocator)
+          curriculum=table, self_play_interval=n, reset="device")  # warm-up (kernels, allocator)
     torch.cuda.synchronize()
     marks = []
     agent, st = train(n_arenas=n, rounds=2, cfg=cfg, device=dev, updates_per_round=1, curriculum=table,
-                      self_play_interval=n,
+                      self_play_interval=n, reset="device",
                       log=lambda r, s: (torch.cuda.synchronize(), marks.append(time.perf_counter())))
     sec = marks[1] - marks[0]  # round 2: the snapshot pool is populated, so the mix includes self-play
     return {"value": n * steps / sec, "unit": "env-steps/s", "arenas": n, "steps": steps,
             "opponents": st["opponents"][1],
-            "sample": f"round 2 of hockey_amd.td3.train on {n} arenas x {steps} steps: actor + noise, opponent "
-                      "mix (strong / weak bot / self-play snapshot), hk_step, replay push, 1 learner update"}
+            "sample": f"round 2 of hockey_amd.td3.train on {n} arenas x {steps} steps: device reset, actor + noise, "
+                      "opponent mix (strong / weak bot / self-play snapshot), hk_step, replay push, 1 learner update"}
 
 
 def main():
