@@ -61,6 +61,10 @@ class HockeyEnv:
         self._rec = torch.zeros(_REC, dtype=torch.uint8, device=self._vec.device)
         self._act = torch.zeros(N.ACT_DIM, dtype=torch.float32, device=self._vec.device)
         self._inc = torch.zeros(2, dtype=torch.float64, device=self._vec.device)
+        # pinned host staging: the per-step transfers are asynchronous copies, one stream sync per step
+        self._rec_h = torch.zeros(_REC, dtype=torch.uint8, pin_memory=True)
+        self._act_h = torch.zeros(N.ACT_DIM, dtype=torch.float32, pin_memory=True)
+        self._inc_h = torch.zeros(2, dtype=torch.float64, pin_memory=True)
         base = self._rec.data_ptr()
         self._io = N.StepIO()
         self._io.actions = self._act.data_ptr()
@@ -103,7 +107,11 @@ class HockeyEnv:
             N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
         N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
         N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
-        b = self._rec.cpu().numpy()
+        import torch
+
+        self._rec_h.copy_(self._rec, non_blocking=True)
+        torch.cuda.current_stream(self._vec.device).synchronize()
+        b = self._rec_h.numpy()
         self._snap = {
             "obs": np.frombuffer(b, np.float32, 18, _OBS).astype(np.float64),
             "obs2": np.frombuffer(b, np.float32, 18, _OBS2).astype(np.float64),
@@ -135,21 +143,18 @@ class HockeyEnv:
         return self._obs_out(s["obs"]), self._get_info()
 
     def _launch_step(self, a8, opp_inc=None):
-        self._act.copy_(self._torch_from(a8))
+        # the previous step ended with a stream sync, so the pinned staging buffers are free to reuse
+        self._act_h.numpy()[:] = a8
+        self._act.copy_(self._act_h, non_blocking=True)
         io = self._io
         io.opp_inc = None
         if opp_inc is not None:
-            self._inc.copy_(self._torch_from(opp_inc))
+            self._inc_h.numpy()[:] = opp_inc
+            self._inc.copy_(self._inc_h, non_blocking=True)
             io.opp_inc = self._inc.data_ptr()
         N.check(self._vec.L.hk_step(self._vec._ctx, ctypes.byref(io), self._vec._stream()), "hk_step")
         s = self._refresh(stepped=True)
         return self._obs_out(s["obs"]), s["reward"], s["done"], False, self._info_dict(s["info"])
-
-    @staticmethod
-    def _torch_from(x):
-        import torch
-
-        return torch.from_numpy(np.ascontiguousarray(x))
 
     def step(self, action):
         a = np.clip(np.asarray(action, np.float64), -1, +1).astype(np.float32)  # hockey_env.py:659
