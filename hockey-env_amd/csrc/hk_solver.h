@@ -508,7 +508,12 @@ static_assert(kVelIters % 4 == 0, "the snapshot period divides the iteration cou
 template <bool kSA, int kP>
 HK_DEV void vone_chunk(FSlot &s, bool dynA, f2 &vA, float &wA, f2 &vB, float &wB, uint32_t (&sn)[10], int &it,
                        int stop, int first, bool &active) {
-  HK_MARK(vone_begin);
+  if constexpr (kSA && kP == 1) HK_MARK(vone_begin_s1);
+  else if constexpr (kSA && kP == 2) HK_MARK(vone_begin_s2);
+  else if constexpr (kSA) HK_MARK(vone_begin_s0);
+  else if constexpr (kP == 1) HK_MARK(vone_begin_d1);
+  else if constexpr (kP == 2) HK_MARK(vone_begin_d2);
+  else HK_MARK(vone_begin_d0);
   for (; it < stop && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -565,22 +570,26 @@ HK_DEV void vone_family(FSlot &s, Dyn &B, int &it, bool &active, int first) {
   }
 }
 
-// Two-contact family (islands of at most two contacts; a one-contact lane runs it with contact 1 masked
-// off).  Each contact keeps its two bodies' velocities in locals; after a contact is solved, the other
-// contact's copy of any body it shares (equal body index) is refreshed from it, so every solve reads exactly
-// the velocities the body-file loop reads, at 2 selects per shared-body component instead of the body file's
+// Two-contact family (at most two live contacts; a one-contact lane runs it with contact 1 masked off).
+// Each contact keeps its two bodies' velocities in locals; after a contact is solved, the other contact's
+// copy of any body it shares (equal body index) is refreshed from it, so every solve reads exactly the
+// velocities the body-file loop reads, at 2 selects per shared-body component instead of the body file's
 // gather and scatter.  A static body A is +0 at every solve, as get_vel_a returns it.  The snapshot covers
 // every island body (each appears in some contact) and both contacts' impulses: the set the general loop
-// compares, some bodies twice.
+// compares, some bodies twice.  When the two contacts belong to different islands (`sep`: no shared
+// dynamic body), each contact's half of the snapshot is its island's whole state, so a contact whose half
+// is periodic retires on its own (on0 / on1 false) while the other keeps iterating (see velocity_iterations).
 HK_DEV f2 sel2(bool c, f2 a, f2 b) { return f2{c ? a[0] : b[0], c ? a[1] : b[1]}; }
 struct TwoState {
   f2 vA0, vB0, vA1, vB1;
   float wA0, wB0, wA1, wB1;
   uint32_t sn[20];
 };
-template <int kP0, int kP1>
-HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool dA0, bool dA1, bool a1a0, bool a1b0,
-                       bool b1a0, bool b1b0, int &it, int stop, int first, bool &active) {
+// kG: some lane has retired contact 0 (it is then skipped by a per-lane branch; otherwise solved unguarded)
+template <int kP0, int kP1, bool kG>
+HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bool dA0, bool dA1, bool a1a0,
+                       bool a1b0, bool b1a0, bool b1b0, int &it, int stop, int first, bool &active, bool &on0,
+                       bool &on1) {
   // the state lives in this function's own locals for the loop (selects between fields of a by-reference
   // struct turn into pointer selects, which keep the struct in scratch memory)
   f2 vA0 = t.vA0, vB0 = t.vB0, vA1 = t.vA1, vB1 = t.vB1;
@@ -592,16 +601,18 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool dA0, bo
   for (; it < stop && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (!dA0) {
-        vA0 = f2{0.0f, 0.0f};
-        wA0 = 0.0f;
+      if (!kG || on0) {
+        if (!dA0) {
+          vA0 = f2{0.0f, 0.0f};
+          wA0 = 0.0f;
+        }
+        fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
+        vA1 = sel2(a1a0, vA0, sel2(a1b0, vB0, vA1));
+        wA1 = a1a0 ? wA0 : (a1b0 ? wB0 : wA1);
+        vB1 = sel2(b1a0, vA0, sel2(b1b0, vB0, vB1));
+        wB1 = b1a0 ? wA0 : (b1b0 ? wB0 : wB1);
       }
-      fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
-      vA1 = sel2(a1a0, vA0, sel2(a1b0, vB0, vA1));
-      wA1 = a1a0 ? wA0 : (a1b0 ? wB0 : wA1);
-      vB1 = sel2(b1a0, vA0, sel2(b1b0, vB0, vB1));
-      wB1 = b1a0 ? wA0 : (b1b0 ? wB0 : wB1);
-      if (two) {
+      if (on1) {
         if (!dA1) {
           vA1 = f2{0.0f, 0.0f};
           wA1 = 0.0f;
@@ -622,13 +633,27 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool dA0, bo
                             dA1 ? __float_as_uint(vA1[1]) : 0u, dA1 ? __float_as_uint(wA1) : 0u,
                             two ? __float_as_uint(s1.ni[0]) : 0u, two ? __float_as_uint(s1.ni[1]) : 0u,
                             two ? __float_as_uint(s1.ti[0]) : 0u, two ? __float_as_uint(s1.ti[1]) : 0u};
-    uint32_t diff = 0u;
+    uint32_t d0 = 0u, d1 = 0u;
 #pragma unroll
-    for (int k = 0; k < 20; ++k) {
-      diff |= x[k] ^ sn[k];
+    for (int k = 0; k < 10; ++k) {
+      d0 |= x[k] ^ sn[k];
       sn[k] = x[k];
     }
-    if (it + 3 >= first && diff == 0u) active = false;
+#pragma unroll
+    for (int k = 10; k < 20; ++k) {
+      d1 |= x[k] ^ sn[k];
+      sn[k] = x[k];
+    }
+    if (it + 3 >= first) {
+      if (sep) {
+        on0 = on0 && d0 != 0u;
+        on1 = on1 && d1 != 0u;
+      } else if ((d0 | d1) == 0u) {
+        on0 = false;
+        on1 = false;
+      }
+      if (!on0 && !on1) active = false;
+    }
   }
   HK_MARK(vtwo_end);
   if (it >= kVelIters) active = false;
@@ -637,14 +662,16 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool dA0, bo
 #pragma unroll
   for (int k = 0; k < 20; ++k) t.sn[k] = sn[k];
 }
-// runs until every lane is done or no running lane has two contacts (then the one-contact family takes over)
-HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, int nc, int &it, bool &active, int first) {
+// runs until every lane is done or no running lane has both contacts live (then the one-contact family takes
+// over).  on0 / on1 in: the lane's contacts that iterate (on1 == two); out: the ones still unfinished.
+HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &active, int first, bool &on0,
+                        bool &on1) {
   const bool entered = active;
-  const bool two = nc == 2;
   const int a0 = fs_bA(s0), b0 = fs_bB(s0);
   const int a1 = two ? fs_bA(s1) : 15, b1 = two ? fs_bB(s1) : 15;  // 15: matches no body
   const bool dA0 = a0 < 3, dA1 = a1 < 3;
   const bool a1a0 = a1 == a0, a1b0 = a1 == b0, b1a0 = b1 == a0, b1b0 = b1 == b0;
+  const bool sep = two && fs_isl(s0) != fs_isl(s1);
   const int vc0 = fs_vcount(s0), vc1 = two ? fs_vcount(s1) : 1;
   TwoState t;
   v2 q;
@@ -658,12 +685,28 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, int nc, int &it, bool &act
   t.vB1 = F2(q);
 #pragma unroll
   for (int k = 0; k < 20; ++k) t.sn[k] = 0u;
-  while (wave_any(active) && wave_any(active && two)) {
+  while (wave_any(active) && wave_any(active && on0 && on1)) {
     const int stop = chunk_end(it);
-    if (!wave_any(active && (vc0 != 1 || vc1 != 1)))
-      vtwo_chunk<1, 1>(s0, s1, t, two, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active);
+    if (wave_any(active && !on0))
+      vtwo_chunk<0, 0, true>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+                             on1);
+    else if (!wave_any(active && (vc0 != 1 || vc1 != 1)))
+      vtwo_chunk<1, 1, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+                              on1);
+    // a wave whose running lanes agree on both point counts runs the rows without the other count's code (a
+    // lane of a one-contact island rides along with contact 1 masked off, whatever kP1 says)
+    else if (!wave_any(active && (vc0 != 1 || (two && vc1 != 2))))
+      vtwo_chunk<1, 2, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+                              on1);
+    else if (!wave_any(active && (vc0 != 2 || (two && vc1 != 1))))
+      vtwo_chunk<2, 1, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+                              on1);
+    else if (!wave_any(active && (vc0 != 2 || (two && vc1 != 2))))
+      vtwo_chunk<2, 2, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+                              on1);
     else
-      vtwo_chunk<0, 0>(s0, s1, t, two, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active);
+      vtwo_chunk<0, 0, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+                              on1);
   }
   if (entered) {
     if (dA0) set_vel_a(B, a0, V2(t.vA0), t.wA0);
@@ -675,26 +718,43 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, int nc, int &it, bool &act
   }
 }
 
-// General family: the slot loop over the body file (any island size, register or HBM slots).  With
-// `leave`, it returns after a chunk once no running lane has more than two contacts.
+// General family: the slot loop over the body file (any island size, register or HBM slots).  Islands
+// share no dynamic body, so each island's state (its bodies' velocities, its contacts' impulses) evolves
+// on its own: an island whose state is periodic retires on its own (its slots leave `live` and are no
+// longer solved; its state at iteration 179 is the current one), while the lane's other islands keep
+// iterating.  With `leave`, it returns after a chunk once no running lane has more than two live contacts.
 template <typename SL>
-HK_DEV void vgen_family(SL &S, Dyn &B, int nc, int &it, bool &active, int first, bool leave) {
+HK_DEV void vgen_family(SL &S, Dyn &B, int nc, uint32_t &live, const int (&isl_of)[3], int &it, bool &active,
+                        int first, bool leave) {
   uint32_t sb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) sb[k] = 0u;
-  S.each(nc, [&](FSlot &s, int) { s.sn[0] = s.sn[1] = s.sn[2] = s.sn[3] = 0u; });
+  uint32_t im0 = 0u, im1 = 0u, im2 = 0u;  // slots of islands 0, 1, 2
+  S.each(nc, [&](FSlot &s, int i) {
+    s.sn[0] = s.sn[1] = s.sn[2] = s.sn[3] = 0u;
+    const int k = fs_isl(s);
+    im0 |= k == 0 ? 1u << i : 0u;
+    im1 |= k == 1 ? 1u << i : 0u;
+    im2 |= k == 2 ? 1u << i : 0u;
+  });
   while (wave_any(active)) {
-    if (leave && !wave_any(active && nc > 2)) return;
+    if (leave && !wave_any(active && __popc(live) > 2)) return;
     const int stop = chunk_end(it);
     HK_MARK(vit_begin);
     for (; it < stop && active; it += 4) {  // 4 iterations per trip: the snapshot period
 #pragma unroll
-      for (int u = 0; u < 4; ++u) S.each(nc, [&](FSlot &s, int) { fslot_solve_velocity(s, B); });
-      uint32_t diff = 0u;
+      for (int u = 0; u < 4; ++u)
+        S.each(nc, [&](FSlot &s, int i) {
+          if ((live >> i) & 1u) fslot_solve_velocity(s, B);
+        });
+      uint32_t d0 = 0u, d1 = 0u, d2 = 0u;  // per-island snapshot differences
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
         const uint32_t x = __float_as_uint(B.vx[b]), y = __float_as_uint(B.vy[b]), z = __float_as_uint(B.w[b]);
-        diff |= (x ^ sb[3 * b]) | (y ^ sb[3 * b + 1]) | (z ^ sb[3 * b + 2]);
+        const uint32_t d = (x ^ sb[3 * b]) | (y ^ sb[3 * b + 1]) | (z ^ sb[3 * b + 2]);
+        d0 |= isl_of[b] == 0 ? d : 0u;
+        d1 |= isl_of[b] == 1 ? d : 0u;
+        d2 |= isl_of[b] == 2 ? d : 0u;
         sb[3 * b] = x;
         sb[3 * b + 1] = y;
         sb[3 * b + 2] = z;
@@ -702,36 +762,90 @@ HK_DEV void vgen_family(SL &S, Dyn &B, int nc, int &it, bool &active, int first,
       S.each(nc, [&](FSlot &s, int) {
         const uint32_t x0 = __float_as_uint(s.ni[0]), x1 = __float_as_uint(s.ni[1]);
         const uint32_t x2 = __float_as_uint(s.ti[0]), x3 = __float_as_uint(s.ti[1]);
-        diff |= (x0 ^ s.sn[0]) | (x1 ^ s.sn[1]) | (x2 ^ s.sn[2]) | (x3 ^ s.sn[3]);
+        const uint32_t d = (x0 ^ s.sn[0]) | (x1 ^ s.sn[1]) | (x2 ^ s.sn[2]) | (x3 ^ s.sn[3]);
+        const int k = fs_isl(s);
+        d0 |= k == 0 ? d : 0u;
+        d1 |= k == 1 ? d : 0u;
+        d2 |= k == 2 ? d : 0u;
         s.sn[0] = x0;
         s.sn[1] = x1;
         s.sn[2] = x2;
         s.sn[3] = x3;
       });
-      if (it + 3 >= first && diff == 0u) active = false;
+      if (it + 3 >= first) {
+        live &= (d0 == 0u ? ~im0 : ~0u) & (d1 == 0u ? ~im1 : ~0u) & (d2 == 0u ? ~im2 : ~0u);
+        if (live == 0u) active = false;
+      }
     }
     HK_MARK(vit_end);
     if (it >= kVelIters) active = false;
   }
 }
 
-// 180 velocity iterations over nc slots, with the exact periodic early exit (register slots: the wave walks
-// the families general -> two -> one as its running lanes allow; HBM slots: the general loop)
+// per-lane exchange of register slots i (compile-time) and j (runtime, j >= i), word by word through selects
+template <int C>
+HK_DEV void slot_swap(RegSlots<C> &S, int i, int j) {
+  uint32_t *a = reinterpret_cast<uint32_t *>(&S.s[i]);
+#pragma unroll
+  for (int q = 0; q < C; ++q) {
+    if (q <= i) continue;
+    uint32_t *b = reinterpret_cast<uint32_t *>(&S.s[q]);
+    const bool sw = j == q;
+#pragma unroll
+    for (int k = 0; k < kSlotWords; ++k) {
+      const uint32_t x = a[k], y = b[k];
+      a[k] = sw ? y : x;
+      b[k] = sw ? x : y;
+    }
+  }
+}
+
+// 180 velocity iterations over nc slots, with the exact periodic early exit.  Register slots: the wave walks
+// the families general -> two -> one as the lanes' LIVE contacts allow (contacts of islands that have not
+// yet become periodic; islands retire one by one, see vgen_family / vtwo_family).  The one- and two-contact
+// families run on slots 0 and 1: a lane whose live contacts sit elsewhere has them swapped there (in slot
+// order, so an island's Gauss-Seidel order is kept) and back afterwards.  HBM slots: the general loop.
+// isl_of[b]: island of dynamic body b (-1: none).
 template <typename SL>
-HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc) {
+HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3]) {
   int it = 0;
+  uint32_t live = nc > 0 ? (1u << nc) - 1u : 0u;
   bool active = nc > 0;
   int first = 7;  // the first comparison against a snapshot taken by this loop (it + 3 == 7)
   if constexpr (SL::kRegister) {
     static_assert(SlotCap<SL>::value >= 2, "the one- and two-contact families use slots 0 and 1");
     while (wave_any(active)) {
-      if (wave_any(active && nc > 2)) vgen_family(S, B, nc, it, active, first, true);
-      else if (wave_any(active && nc > 1)) vtwo_family(S.s[0], S.s[1], B, nc, it, active, first);
-      else vone_family(S.s[0], B, it, active, first);
+      const int nl = __popc(live);
+      if (wave_any(active && nl > 2)) {
+        vgen_family(S, B, nc, live, isl_of, it, active, first, true);
+      } else {
+        const bool fam2 = wave_any(active && nl > 1);
+        const int j0 = nl > 0 ? __ffs(live) - 1 : 0;
+        const int j1 = nl > 1 ? __ffs(live & (live - 1u)) - 1 : 1;
+        const bool perm = wave_any(active && (j0 != 0 || (fam2 && j1 != 1)));
+        if (perm) {
+          slot_swap(S, 0, j0);
+          if (fam2) slot_swap(S, 1, j1);
+        }
+        if (fam2) {
+          bool on0 = active, on1 = active && nl > 1;
+          vtwo_family(S.s[0], S.s[1], B, nl > 1, it, active, first, on0, on1);
+          live &= (on0 ? ~0u : ~(1u << j0)) & (nl > 1 && !on1 ? ~(1u << j1) : ~0u);
+        } else {
+          const bool entered = active;
+          vone_family(S.s[0], B, it, active, first);
+          live = entered ? 0u : live;
+        }
+        if (perm) {
+          if (fam2) slot_swap(S, 1, j1);
+          slot_swap(S, 0, j0);
+        }
+      }
+      active = live != 0u && it < kVelIters;
       first = it + 7;  // the next family starts a fresh snapshot
     }
   } else {
-    vgen_family(S, B, nc, it, active, first, false);
+    vgen_family(S, B, nc, live, isl_of, it, active, first, false);
   }
   return it;
 }

@@ -20,6 +20,7 @@ static inline unsigned __float_as_uint(float x) { unsigned r; std::memcpy(&r, &x
 static inline float __int_as_float(int x) { float r; std::memcpy(&r, &x, 4); return r; }
 static inline float __uint_as_float(unsigned x) { float r; std::memcpy(&r, &x, 4); return r; }
 static inline int __ffs(unsigned x) { return __builtin_ffs((int)x); }
+static inline int __popc(unsigned x) { return __builtin_popcount(x); }
 static inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 static inline int __double2hiint(double d) { uint64_t u; std::memcpy(&u, &d, 8); return (int)(u >> 32); }
 static inline double __hiloint2double(int hi, int lo) {

@@ -62,3 +62,25 @@ for k, nm in enumerate(names):
         m = lanes[:, :, :, k].max(2).reshape(-1)
         c = np.corrcoef(m, flat)[0, 1] if m.std() > 0 else 0
         print(f"corr(wave cycles, wave-max {nm}) = {c:.2f}")
+# island velocity cycles of a wave against its slowest lane's island solve (iterations, contacts)
+vel = ph[:, :, 3].reshape(-1)
+W = lanes.reshape(-1, 64, 24)
+vmax = W[:, :, 2].max(1)
+print("isl-velocity cycles per wave by the wave's longest island solve:")
+for lo, hi in ((0, 9), (9, 17), (17, 100), (100, 179), (180, 181)):
+    m = (vmax >= lo) & (vmax < hi)
+    if m.any():
+        print(f"  max vit_isl [{lo},{hi}): waves {m.mean() * 100:6.2f}%  cycles mean {vel[m].mean():9.0f}  "
+              f"p90 {np.percentile(vel[m], 90):9.0f}  max {vel[m].max():9.0f}")
+full = W[:, :, 2] >= 180
+ncl = np.where(full, W[:, :, 6], -1).max(1)  # contacts of the lanes that ran 180 iterations
+for c in range(1, 5):
+    m = ncl == c
+    if m.any():
+        print(f"  waves whose 180-iteration lanes have at most {c} contacts: {m.sum():6d}  cycles mean {vel[m].mean():9.0f}"
+              f"  per iteration {vel[m].mean() / 180:7.0f}")
+nfull = full.sum(1)
+for c in (1, 2, 3):
+    m = nfull == c
+    if m.any():
+        print(f"  waves with {c} lanes at 180: {m.sum():6d}  cycles mean {vel[m].mean():9.0f}")
