@@ -660,7 +660,7 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
   });
   S.each(nc, [&](FSlot &s, int) { fslot_warm_start(s, w.d); });
   HK_TIC(T, 2);  // diagnostics: island setup (DFS, integrate, constraint init, warm start)
-  const int vit = velocity_iterations(S, w.d, nc, island_of);
+  const int vit = velocity_iterations(S, w.d, nc, island_of, T);
   HK_TIC(T, 3);  // diagnostics: velocity iterations
 #ifdef HK_PHASE_TIMERS
   w.dg_vit_isl += vit;
@@ -749,7 +749,7 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
   place(w.d.a0, db, pick(w.d.a, db, 0.0f));
   S.each(nc, [&](FSlot &s, int) { fslot_init_velocity(s, w); });
   const int isl_of[3] = {db == 0 ? 0 : -1, db == 1 ? 0 : -1, db == 2 ? 0 : -1};  // one island: B
-  const int vit = velocity_iterations(S, w.d, nc, isl_of);
+  const int vit = velocity_iterations(S, w.d, nc, isl_of, T);
   HK_TIC(T, 11);  // diagnostics: TOI velocity iterations
 #ifdef HK_PHASE_TIMERS
   w.dg_vit_toi += vit;

@@ -250,8 +250,10 @@ HK_DEV bool wave_any(bool p) { return p; }
 // Diagnostic build only (make TIMERS=1): per-phase shader-clock accounting; compiled out otherwise.
 #ifdef HK_PHASE_TIMERS
 struct PhaseT {
-  unsigned long long last, acc[13];
+  unsigned long long last, acc[13], fam[3];  // fam: velocity-loop cycles in the general / two / one families
 };
+#define HK_FAM_T0() const unsigned long long _ft0 = __builtin_amdgcn_s_memtime()
+#define HK_FAM_ADD(T, k) ((T).fam[k] += __builtin_amdgcn_s_memtime() - _ft0)
 #define HK_TIC(T, k)                                              \
   do {                                                            \
     unsigned long long _t = __builtin_amdgcn_s_memtime();         \
@@ -261,6 +263,8 @@ struct PhaseT {
 #else
 struct PhaseT {};
 #define HK_TIC(T, k) ((void)0)
+#define HK_FAM_T0() ((void)0)
+#define HK_FAM_ADD(T, k) ((void)0)
 #endif
 
 }  // namespace hk

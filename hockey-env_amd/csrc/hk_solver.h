@@ -807,7 +807,7 @@ HK_DEV void slot_swap(RegSlots<C> &S, int i, int j) {
 // order, so an island's Gauss-Seidel order is kept) and back afterwards.  HBM slots: the general loop.
 // isl_of[b]: island of dynamic body b (-1: none).
 template <typename SL>
-HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3]) {
+HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3], PhaseT &T) {
   int it = 0;
   uint32_t live = nc > 0 ? (1u << nc) - 1u : 0u;
   bool active = nc > 0;
@@ -816,8 +816,10 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3]) {
     static_assert(SlotCap<SL>::value >= 2, "the one- and two-contact families use slots 0 and 1");
     while (wave_any(active)) {
       const int nl = __popc(live);
+      HK_FAM_T0();
       if (wave_any(active && nl > 2)) {
         vgen_family(S, B, nc, live, isl_of, it, active, first, true);
+        HK_FAM_ADD(T, 0);
       } else {
         const bool fam2 = wave_any(active && nl > 1);
         const int j0 = nl > 0 ? __ffs(live) - 1 : 0;
@@ -831,10 +833,12 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3]) {
           bool on0 = active, on1 = active && nl > 1;
           vtwo_family(S.s[0], S.s[1], B, nl > 1, it, active, first, on0, on1);
           live &= (on0 ? ~0u : ~(1u << j0)) & (nl > 1 && !on1 ? ~(1u << j1) : ~0u);
+          HK_FAM_ADD(T, 1);
         } else {
           const bool entered = active;
           vone_family(S.s[0], B, it, active, first);
           live = entered ? 0u : live;
+          HK_FAM_ADD(T, 2);
         }
         if (perm) {
           if (fam2) slot_swap(S, 1, j1);

@@ -362,6 +362,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     float *d = io.debug + a * 24;
     d[1] = (float)w.n_toi; d[2] = (float)w.dg_vit_isl; d[3] = (float)w.dg_vit_toi; d[4] = (float)w.dg_pit;
     d[5] = (float)w.dg_toi_calls; d[6] = (float)w.dg_nc_max; d[7] = (float)w.n_big;
+    d[21] = (float)T.fam[0]; d[22] = (float)T.fam[1]; d[23] = (float)T.fam[2];
   }
 #endif
 }

@@ -84,3 +84,8 @@ for c in (1, 2, 3):
     m = nfull == c
     if m.any():
         print(f"  waves with {c} lanes at 180: {m.sum():6d}  cycles mean {vel[m].mean():9.0f}")
+# velocity-loop family cycles (d[21..23], island + TOI solves) in the slowest wave of each step vs the mean wave
+fam = D[:, ::64, 21:24]
+sf = fam[np.arange(steps), wave.argmax(1)]
+print("velocity families (general / two / one), cycles: mean wave", fam.mean((0, 1)).round(0).tolist(),
+      " slowest wave", sf.mean(0).round(0).tolist())
