@@ -11,6 +11,15 @@
 
 namespace hk {
 
+// Host harness only (hostcheck, HK_HOST_DIAG): how often the velocity loop's island retirement and slot swaps
+// ran, so a CPU test can show that its lockstep runs exercised them.  [0] an island retired while another
+// of its lane's islands kept iterating, [1] a lane's live contacts were swapped into slots 0/1.
+#ifdef HK_HOST_DIAG
+extern unsigned long long g_hk_host_diag[4];
+#define HK_HOST_DIAG_INC(k) (++g_hk_host_diag[k])
+#else
+#define HK_HOST_DIAG_INC(k) ((void)0)
+#endif
 
 
 // One contact of the solver.  Only what the velocity iterations touch lives here (36 words); the
@@ -648,6 +657,7 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bo
       if (sep) {
         on0 = on0 && d0 != 0u;
         on1 = on1 && d1 != 0u;
+        if (on0 != on1) HK_HOST_DIAG_INC(0);
       } else if ((d0 | d1) == 0u) {
         on0 = false;
         on1 = false;
@@ -773,8 +783,10 @@ HK_DEV void vgen_family(SL &S, Dyn &B, int nc, uint32_t &live, const int (&isl_o
         s.sn[3] = x3;
       });
       if (it + 3 >= first) {
+        const uint32_t before = live;
         live &= (d0 == 0u ? ~im0 : ~0u) & (d1 == 0u ? ~im1 : ~0u) & (d2 == 0u ? ~im2 : ~0u);
         if (live == 0u) active = false;
+        else if (live != before) HK_HOST_DIAG_INC(0);
       }
     }
     HK_MARK(vit_end);
@@ -826,6 +838,7 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3], Ph
         const int j1 = nl > 1 ? __ffs(live & (live - 1u)) - 1 : 1;
         const bool perm = wave_any(active && (j0 != 0 || (fam2 && j1 != 1)));
         if (perm) {
+          if (active && (j0 != 0 || (fam2 && j1 != 1))) HK_HOST_DIAG_INC(1);
           slot_swap(S, 0, j0);
           if (fam2) slot_swap(S, 1, j1);
         }

@@ -30,6 +30,7 @@ static inline double __hiloint2double(int hi, int lo) {
   return d;
 }
 
+#define HK_HOST_DIAG
 #include "../hk_core.h"
 
 constexpr hk::Scene g_scene =  // the kernels' compile-time scene (hk_scene_gen.cpp)
@@ -38,6 +39,8 @@ constexpr hk::Scene g_scene =  // the kernels' compile-time scene (hk_scene_gen.
 
 #define SLDS g_scene  // the host build reads the one scene copy
 #include "../hk_step.h"
+
+unsigned long long hk::g_hk_host_diag[4];
 
 using namespace hk;
 
@@ -132,6 +135,12 @@ void hkh_raw(void *h, float **f, int32_t **i) {
   HostCtx *c = (HostCtx *)h;
   *f = c->f.data();
   *i = c->i.data();
+}
+
+// velocity-loop coverage counters (hk_solver.h HK_HOST_DIAG_INC), process-wide; read and cleared
+void hkh_diag(unsigned long long *out4) {
+  std::memcpy(out4, hk::g_hk_host_diag, sizeof(hk::g_hk_host_diag));
+  std::memset(hk::g_hk_host_diag, 0, sizeof(hk::g_hk_host_diag));
 }
 
 void hkh_counters(void *h, unsigned long long *out16) {

@@ -35,8 +35,18 @@ def lib():
                         ("hkh_set_state", 4), ("hkh_observe", 3), ("hkh_counters", 2)):
             getattr(L, name).restype = None
             getattr(L, name).argtypes = [vp] * n
+        L.hkh_diag.restype = None
+        L.hkh_diag.argtypes = [vp]
         _lib = L
     return _lib
+
+
+def velocity_diag():
+    """Velocity-loop coverage counters of the host build since the last call (and clears them): [0] islands
+    retired while another island of the lane kept iterating, [1] live contacts swapped into slots 0/1."""
+    out = np.zeros(4, np.uint64)
+    lib().hkh_diag(out.ctypes.data)
+    return out
 
 
 def _p(a):

@@ -12,7 +12,7 @@ import pytest
 
 from hockey_amd.placement import np_random, placement
 
-from hostcheck import HostVec
+from hostcheck import HostVec, velocity_diag
 
 
 def _f32(x):
@@ -140,3 +140,14 @@ def test_per_step_opponent_mix_vs_oracle_vec(oracle):
     assert "field" not in out, out
     out = _vec_lockstep(oracle, 32, 200, 1, ("strong", "weak"), seed=24, external=True, mix=True)
     assert "field" not in out, out
+
+
+def test_island_retirement_and_slot_swaps_vs_oracle(oracle):
+    """Islands of one lane retire one by one inside the shared velocity loop (hk_solver.h vgen / vtwo), and
+    the live contacts are swapped into the one- and two-contact slots: both paths run in a bit-exact lockstep
+    of the strong-vs-strong workload against the oracle (which solves island by island, like Box2D)."""
+    velocity_diag()
+    out = _vec_lockstep(oracle, 256, 400, 0, ("strong", "strong"), seed=31)
+    assert "field" not in out, out
+    d = velocity_diag()
+    assert d[0] > 0 and d[1] > 0, d
