@@ -59,6 +59,9 @@ def _args():
     ap.add_argument("--c5-steps", type=int, default=50,
                     help="also time one C5 TD3 collection round (65 536 arenas, opponent mix) of this many steps "
                          "(0 = skip); reported under 'c5_collect'")
+    ap.add_argument("--c4-steps", type=int, default=100,
+                    help="also time BASELINE C4's per-GPU shard (2x --arenas, random rollouts) this many steps "
+                         "(0 = skip); reported under 'c4_shard'")
     ap.add_argument("--streams", type=int, default=2,
                     help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
                          "reported under 'streams'")
@@ -289,6 +292,38 @@ def time_c5(n, steps, dev):
                       "opponent mix (strong / weak bot / self-play snapshot), hk_step, replay push, 1 learner update"}
 
 
+def time_c4(n, steps, preroll_steps, seed, dev):
+    """BASELINE C4's per-GPU shard: n (131 072) arenas on one GPU, random-vs-random rollouts (U(-1,1) actions
+    drawn in the kernel), auto-reset, one hk_step launch per step after a pre-roll past the first episodes.
+    With twice as many waves as SIMDs, a SIMD whose first wave finishes early starts a queued one, so a
+    launch is paced less by any single slow wave than at 65 536 arenas."""
+    import torch
+
+    from hockey_amd import _native as N
+    from hockey_amd.vec_env import VecHockeyEnv
+
+    env = VecHockeyEnv(n, device=dev, policies=("random", "random"), auto_reset=True, seed=seed,
+                       arena_offset=0)
+    env.reset()
+    preroll(env, preroll_steps, N)
+    io = N.StepIO()
+    io.obs, io.reward, io.done, io.info = (env.obs_buf.data_ptr(), env.reward_buf.data_ptr(),
+                                           env.done_buf.data_ptr(), env.info_buf.data_ptr())
+    for _ in range(20):
+        env.step_raw(io)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        env.step_raw(io)
+    torch.cuda.synchronize()
+    sec = time.perf_counter() - t0
+    env.close()
+    return {"value": n * steps / sec, "unit": "env-steps/s", "arenas": n, "steps": steps,
+            "ms_per_step": sec / steps * 1e3,
+            "sample": f"BASELINE C4 per-GPU shard: {n} arenas, random-vs-random (in-kernel U(-1,1)), auto-reset, "
+                      f"{steps} hk_step launches after a {preroll_steps}-step pre-roll"}
+
+
 def main():
     args = _args()
     import torch
@@ -409,6 +444,11 @@ def main():
                 line["c5_collect"] = time_c5(n, args.c5_steps, dev)
             except Exception as e:  # noqa: BLE001
                 line["c5_collect"] = {"error": repr(e)[:300]}
+        if world == 1 and args.c4_steps > 0:
+            try:
+                line["c4_shard"] = time_c4(2 * n, args.c4_steps, args.preroll, args.seed, dev)
+            except Exception as e:  # noqa: BLE001
+                line["c4_shard"] = {"error": repr(e)[:300]}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_preroll, args.cpu_steps,
                                                 args.seed)

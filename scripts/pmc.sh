@@ -4,7 +4,7 @@
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---no-cpu-baseline --rollout 0 --streams 0 --facade-steps 0 --c5-steps 0 --steps 40 --warmup 20}
+ARGS=${BENCH_ARGS:---no-cpu-baseline --rollout 0 --streams 0 --facade-steps 0 --c5-steps 0 --c4-steps 0 --steps 40 --warmup 20}
 for C in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/pmc_$C
   timeout -k 10 600 rocprofv3 --pmc $C -d gpurun_out/pmc_$C -o run --output-format csv -- \

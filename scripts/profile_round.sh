@@ -18,7 +18,7 @@ timeout -k 10 300 python bench.py > $O/bench.log 2>&1
 tail -1 $O/bench.log
 rm -rf gpurun_out/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --streams 0 --rollout 0 --facade-steps 0 --c5-steps 0 > $O/prof_bench.log 2>&1
+  python3 bench.py --no-cpu-baseline --streams 0 --rollout 0 --facade-steps 0 --c5-steps 0 --c4-steps 0 > $O/prof_bench.log 2>&1
 find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 find gpurun_out/prof -name "*kernel_trace.csv" -exec cp {} $O/kernel_trace.csv \;
 tail -1 $O/prof_bench.log

@@ -4,7 +4,7 @@
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---no-cpu-baseline --rollout 0 --streams 0 --facade-steps 0 --c5-steps 0 --steps 40 --warmup 20}
+ARGS=${BENCH_ARGS:---no-cpu-baseline --rollout 0 --streams 0 --facade-steps 0 --c5-steps 0 --c4-steps 0 --steps 40 --warmup 20}
 P1=${P1-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_BUSY_CYCLES"}
 P2=${P2-"SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES"}
 P3=${P3-}
