@@ -62,6 +62,9 @@ def _args():
     ap.add_argument("--c4-steps", type=int, default=100,
                     help="also time BASELINE C4's per-GPU shard (2x --arenas, random rollouts) this many steps "
                          "(0 = skip); reported under 'c4_shard'")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU-only rehearsal of the multi-rank path (gloo, no simulation): launcher, barrier, "
+                         "max-over-ranks timing and the line format; the line carries \"rehearsal\": true")
     ap.add_argument("--streams", type=int, default=2,
                     help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
                          "reported under 'streams'")
@@ -324,64 +327,147 @@ def time_c4(n, steps, preroll_steps, seed, dev):
                       f"{steps} hk_step launches after a {preroll_steps}-step pre-roll"}
 
 
+def launch_ranks(args):
+    """`--gpus N` without a torch.distributed launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set like torch.distributed.run) BEFORE this process touches any
+    GPU, wait for all of them, and return non-zero if any rank failed.  Rank 0 prints the bench line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+class RehearsalEnv:
+    """--rehearse: a CPU stand-in for one rank's arena shard (no GPU, gloo collectives).  It runs the launcher,
+    the barrier / max-over-ranks timing and the line format of the real bench on a CPU-only host; its
+    step_raw does no simulation and the line it yields says so ("rehearsal": true)."""
+
+    def __init__(self, n):
+        self.n = n
+        self.steps = 0
+
+    def step_raw(self, io):
+        self.steps += self.n
+
+    def rollout_raw(self, k, io):
+        self.steps += self.n * k
+
+    def reset_counters(self):
+        self.steps = 0
+
+    def counters(self):
+        c = [0] * 16
+        c[0], c[1] = self.steps, 1
+        return c
+
+    def bytes_per_step(self):
+        return 285, 0
+
+    def close(self):
+        pass
+
+
+def provenance():
+    """Which code the numbers describe: the library's build hash (its .srchash sidecar), the hash of the
+    sources in this tree, and whether the committed counter summaries were collected at that same hash."""
+    from hockey_amd._native import built_hash, source_hash
+
+    return built_hash(), source_hash()
+
+
 def main():
     args = _args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))  # before `import torch` / any GPU call in this process
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.arenas <= 0 or args.steps <= 0:
+        sys.exit(f"bench.py: rank {rank}: --arenas and --steps must be positive")
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = not args.rehearse
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if gpu:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend="gloo")
+    if gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        sync = torch.cuda.synchronize
+    else:
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
 
     from hockey_amd import _native as N
-    from hockey_amd.vec_env import VecHockeyEnv
 
     n = args.arenas
     pol = ("strong", "strong") if args.policy == "basic" else ("random", "random")
-    env = VecHockeyEnv(n, device=dev, policies=pol, auto_reset=True, seed=args.seed,
-                       arena_offset=shard_offset(rank, n))
-    env.reset()
     io = N.StepIO()
-    io.obs = env.obs_buf.data_ptr()
-    io.reward = env.reward_buf.data_ptr()
-    io.done = env.done_buf.data_ptr()
-    io.info = env.info_buf.data_ptr()
+    if gpu:
+        from hockey_amd.vec_env import VecHockeyEnv
+
+        env = VecHockeyEnv(n, device=dev, policies=pol, auto_reset=True, seed=args.seed,
+                           arena_offset=shard_offset(rank, n))
+        env.reset()
+        io.obs = env.obs_buf.data_ptr()
+        io.reward = env.reward_buf.data_ptr()
+        io.done = env.done_buf.data_ptr()
+        io.info = env.info_buf.data_ptr()
+    else:
+        env = RehearsalEnv(n)
 
     preroll(env, args.preroll, N)
     for _ in range(args.warmup):
         env.step_raw(io)
-    torch.cuda.synchronize()
+    sync()
     env.reset_counters()
-    stream = torch.cuda.current_stream(dev)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if gpu:
+        stream = torch.cuda.current_stream(dev)
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        starts[k].record(stream)
+        if gpu:
+            starts[k].record(stream)
         env.step_raw(io)
-        ends[k].record(stream)
-    torch.cuda.synchronize()
+        if gpu:
+            ends[k].record(stream)
+    sync()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+    kern_ms = (sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps) if gpu else elapsed / args.steps * 1e3
     cnt = env.counters()
     if world > 1:
         elapsed, cnt = reduce_over_ranks(elapsed, cnt, dist, dev)
-    rollout = None
-    if args.rollout > 1:
+    rollout = streams = None
+    if gpu and args.rollout > 1:
         rollout = _time_rollout(env, N, torch, dist, world, dev, args)
-    streams = None
-    if args.streams > 1:
+    if gpu and args.streams > 1:
         streams = _time_streams(args, N, torch, dist, world, rank, dev, pol)
     total_steps = n * world * args.steps
     assert int(cnt[N.CNT_STEPS]) == total_steps, (cnt, total_steps)
@@ -395,6 +481,8 @@ def main():
         key = f"{args.policy}_{n}"
         pmc = _profile("pmc_summary.json", key) or {}
         sq = _profile("sq_summary.json", key) or {}
+        lib_hash, src_hash = provenance()
+        stale = (sq.get("source_hash") != lib_hash or pmc.get("source_hash") != lib_hash or lib_hash != src_hash)
         lane_ops = sq.get("valu_lane_ops_per_launch")
         valu_tops = lane_ops / (kern_ms * 1e-3) / 1e12 if lane_ops else None
         line = {
@@ -421,6 +509,9 @@ def main():
                          "valu_lane_ops_per_launch": lane_ops,
                          "valu_issue_util": sq.get("valu_issue_util"), "valu_lane_util": sq.get("valu_lane_util"),
                          "counters_from": sq.get("source"),
+                         "library_hash": lib_hash, "source_hash": src_hash,
+                         "counters_hash": {"sq": sq.get("source_hash"), "pmc": pmc.get("source_hash")},
+                         "counters_stale": bool(stale),
                          "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": hbm_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": alg_bytes,
                                  "traffic_bytes_per_launch": pmc.get("hbm_bytes_per_launch"),
@@ -429,27 +520,30 @@ def main():
             "episodes": int(cnt[N.CNT_EPISODES]),
             "toi_events": int(cnt[N.CNT_TOI]),
         }
+        if not gpu:
+            line["rehearsal"] = True
+            line["data"] = "REHEARSAL on CPU (gloo): no simulation ran; launcher / timing / line format only"
         if rollout is not None:
             line["rollout"] = rollout
         if streams is not None:
             line["streams"] = streams
         # side legs: reported beside the headline, never allowed to take the bench line down with them
-        if world == 1 and args.facade_steps > 0:
+        if gpu and world == 1 and args.facade_steps > 0:
             try:
                 line["facade_single_env"] = time_facade(args.facade_steps, dev)
             except Exception as e:  # noqa: BLE001
                 line["facade_single_env"] = {"error": repr(e)[:300]}
-        if world == 1 and args.c5_steps > 0:
+        if gpu and world == 1 and args.c5_steps > 0:
             try:
-                line["c5_collect"] = time_c5(n, args.c5_steps, dev)
+                line["c5_round"] = time_c5(n, args.c5_steps, dev)
             except Exception as e:  # noqa: BLE001
-                line["c5_collect"] = {"error": repr(e)[:300]}
-        if world == 1 and args.c4_steps > 0:
+                line["c5_round"] = {"error": repr(e)[:300]}
+        if gpu and world == 1 and args.c4_steps > 0:
             try:
                 line["c4_shard"] = time_c4(2 * n, args.c4_steps, args.preroll, args.seed, dev)
             except Exception as e:  # noqa: BLE001
                 line["c4_shard"] = {"error": repr(e)[:300]}
-        if world == 1 and not args.no_cpu_baseline:
+        if gpu and world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.policy, args.cpu_arenas, args.cpu_preroll, args.cpu_steps,
                                                 args.seed)
         print(json.dumps(line), flush=True)

@@ -156,6 +156,8 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
   Ctx *c = (Ctx *)ctx;
   if (!io->actions && (c->cfg.policy[0] == HK_POLICY_EXTERNAL || c->cfg.policy[1] == HK_POLICY_EXTERNAL))
     return fail(HK_E_INVALID, "%s: a player takes external actions but io->actions is NULL", who);
+  if (io->policy2 && !io->actions)  // an override may pick HK_POLICY_EXTERNAL for any arena
+    return fail(HK_E_INVALID, "%s: io->policy2 is given but io->actions is NULL", who);
   hk::StepIO s;
   s.actions = io->actions;
   s.opp_inc = io->opp_inc;
@@ -219,8 +221,7 @@ int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
   hipError_t e = hipSuccess;
-  const size_t bytes = (size_t)c->s.n * 2 * sizeof(double);
-  // device layout is [2][N] (player-major); the ABI layout is [N,2]
+  // device layout is [3][N] (player-major); the ABI layout is [N,2]
   if (phase_out)
     e = hipMemcpy2DAsync(phase_out, 2 * sizeof(double), c->s.phase, sizeof(double), sizeof(double), c->s.n,
                          hipMemcpyDeviceToDevice, (hipStream_t)stream);
@@ -233,8 +234,22 @@ int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void
   if (e == hipSuccess && phase_in)
     e = hipMemcpy2DAsync(c->s.phase + c->s.n, sizeof(double), phase_in + 1, 2 * sizeof(double), sizeof(double),
                          c->s.n, hipMemcpyDeviceToDevice, (hipStream_t)stream);
-  (void)bytes;
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_opponent_phase");
+}
+
+int hk_opponent_phase3(void *ctx, double *phase_out, const double *phase_in, void *stream) {
+  if (!ctx) return fail(HK_E_INVALID, "hk_opponent_phase3: ctx is NULL%s");
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  hipError_t e = hipSuccess;
+  // device layout is [3][N] (row-major by phase row); the ABI layout is [N,3]
+  for (int r = 0; r < 3 && e == hipSuccess && phase_out; ++r)
+    e = hipMemcpy2DAsync(phase_out + r, 3 * sizeof(double), c->s.phase + (size_t)r * c->s.n, sizeof(double),
+                         sizeof(double), c->s.n, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  for (int r = 0; r < 3 && e == hipSuccess && phase_in; ++r)
+    e = hipMemcpy2DAsync(c->s.phase + (size_t)r * c->s.n, sizeof(double), phase_in + r, 3 * sizeof(double),
+                         sizeof(double), c->s.n, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  return e == hipSuccess ? HK_OK : hipfail(e, "hk_opponent_phase3");
 }
 
 int hk_counters(void *ctx, int64_t *out, void *stream) {

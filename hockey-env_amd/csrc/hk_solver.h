@@ -476,12 +476,14 @@ struct HbmSlots {
 #pragma unroll 1
     for (int i = 0; i < nc; ++i) {
       FSlot t;
-      uint32_t *tw = reinterpret_cast<uint32_t *>(&t);
+      float tw[kSlotWords];
 #pragma unroll
-      for (int k = 0; k < kSlotWords; ++k) tw[k] = __float_as_uint(word(i, k));
+      for (int k = 0; k < kSlotWords; ++k) tw[k] = word(i, k);
+      __builtin_memcpy(&t, tw, sizeof(FSlot));
       fn(t, i);
+      __builtin_memcpy(tw, &t, sizeof(FSlot));
 #pragma unroll
-      for (int k = 0; k < kSlotWords; ++k) word(i, k) = __uint_as_float(tw[k]);
+      for (int k = 0; k < kSlotWords; ++k) word(i, k) = tw[k];
     }
   }
   HK_DEV void set_pair(int nc, int p, int isl) {
@@ -794,14 +796,19 @@ HK_DEV void vgen_family(SL &S, Dyn &B, int nc, uint32_t &live, const int (&isl_o
   }
 }
 
-// per-lane exchange of register slots i (compile-time) and j (runtime, j >= i), word by word through selects
+// per-lane exchange of register slots i (compile-time) and j (runtime, j >= i), word by word through selects.
+// The words are copied out and back with memcpy (no type-punned pointer: strict-aliasing clean on the host and
+// sanitizer builds; SROA keeps every word in a register on the device).
 template <int C>
 HK_DEV void slot_swap(RegSlots<C> &S, int i, int j) {
-  uint32_t *a = reinterpret_cast<uint32_t *>(&S.s[i]);
+  static_assert(sizeof(FSlot) == kSlotWords * 4, "FSlot is kSlotWords words");
+  uint32_t a[kSlotWords];
+  __builtin_memcpy(a, &S.s[i], sizeof(FSlot));
 #pragma unroll
   for (int q = 0; q < C; ++q) {
     if (q <= i) continue;
-    uint32_t *b = reinterpret_cast<uint32_t *>(&S.s[q]);
+    uint32_t b[kSlotWords];
+    __builtin_memcpy(b, &S.s[q], sizeof(FSlot));
     const bool sw = j == q;
 #pragma unroll
     for (int k = 0; k < kSlotWords; ++k) {
@@ -809,7 +816,9 @@ HK_DEV void slot_swap(RegSlots<C> &S, int i, int j) {
       a[k] = sw ? y : x;
       b[k] = sw ? x : y;
     }
+    __builtin_memcpy(&S.s[q], b, sizeof(FSlot));
   }
+  __builtin_memcpy(&S.s[i], a, sizeof(FSlot));
 }
 
 // 180 velocity iterations over nc slots, with the exact periodic early exit.  Register slots: the wave walks

@@ -243,7 +243,7 @@ HK_DEV void reset_lane(const DevState &s, const KCfg &cfg, int64_t a, const floa
 }
 
 // One HockeyEnv.step of arena a (policy actions, pre-solve laws, world.Step, outputs, then auto-reset).
-struct LaneOut { int done_edge, win1, win2, ntoi, ovf, nbig; };
+struct LaneOut { int done_edge, win1, win2, ntoi, ovf, nbig, bad_policy; };
 
 HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int64_t a, float *lds, int lane,
                       PhaseT &T, LaneOut &out) {
@@ -256,14 +256,19 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   const uint32_t stepc = (uint32_t)I(s, I_STEP, a);
   // ---- actions: external / Philox random / fused BasicOpponent ----
   float a8[8];
+  int bad_policy = 0;
   for (int p = 0; p < 2; ++p) {
     int pol = cfg.policy[p], row = p;  // row: the acting BasicOpponent's phase (DevState::phase)
     if (p == 1 && io.policy2) {
       pol = io.policy2[a];
       row = pol == 2 ? 2 : 1;
+      if (pol > 3) {  // not an HK_POLICY_*: counted (HK_CNT_BAD_POLICY), the player acts with zeros
+        bad_policy = 1;
+        pol = -1;
+      }
     }
-    if (pol == 0) {
-      for (int k = 0; k < 4; ++k) a8[4 * p + k] = io.actions ? io.actions[a * 8 + 4 * p + k] : 0.0f;
+    if (pol <= 0) {
+      for (int k = 0; k < 4; ++k) a8[4 * p + k] = (io.actions && pol == 0) ? io.actions[a * 8 + 4 * p + k] : 0.0f;
     } else if (pol == 1) {
       const int64_t ga = cfg.arena_offset + a;
       U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), stepc, RNG_ACTION + 0x10 * p);
@@ -357,6 +362,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   out.ntoi = w.n_toi;
   out.ovf = w.overflow;
   out.nbig = w.n_big;
+  out.bad_policy = bad_policy;
 #ifdef HK_PHASE_TIMERS
   if (io.debug) {  // diagnostics build: per-lane work counters
     float *d = io.debug + a * 24;

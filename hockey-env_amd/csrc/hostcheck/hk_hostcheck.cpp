@@ -111,6 +111,7 @@ void hkh_step(void *h, const StepIO *io) {
     c->counters[4] += out.ntoi;
     c->counters[5] += out.ovf;
     c->counters[6] += out.nbig;
+    c->counters[7] += out.bad_policy;
   }
 }
 

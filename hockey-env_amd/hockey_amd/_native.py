@@ -17,7 +17,7 @@ OBS_DIM, ACT_DIM, INFO_DIM, STATE_DIM, AUX_DIM, PARAM_DIM, DEBUG_DIM, NUM_COUNTE
 POLICY_EXTERNAL, POLICY_RANDOM, POLICY_BASIC_WEAK, POLICY_BASIC_STRONG = 0, 1, 2, 3
 STEP_SKIP_PHYSICS = 1
 DIAG_LARGE_ISLANDS = 1
-CNT_STEPS, CNT_EPISODES, CNT_GOALS_P1, CNT_GOALS_P2, CNT_TOI, CNT_OVERFLOW = range(6)
+CNT_STEPS, CNT_EPISODES, CNT_GOALS_P1, CNT_GOALS_P2, CNT_TOI, CNT_OVERFLOW, CNT_LARGE_ISLANDS, CNT_BAD_POLICY = range(8)
 
 
 class HockeyNativeError(RuntimeError):
@@ -39,11 +39,36 @@ class StepIO(ctypes.Structure):
 
 
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",
-           "hk_step", "hk_rollout", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_observe", "hk_counters",
+           "hk_step", "hk_rollout", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_opponent_phase3",
+           "hk_observe", "hk_counters",
            "hk_reset_counters",
            "hk_bytes_per_step", "hk_info"]
 
 _lib = None
+
+# the files csrc/Makefile hashes into <lib>.srchash (HASHSRC = $(SRC) $(HDR) Makefile), in its order
+HASH_SOURCES = ["hk_kernels.hip", "hk_capi.cpp", "hk_core.h", "hk_geom.h", "hk_arena.h", "hk_solver.h", "hk_step.h",
+                "hk_kernels.h", "hk_scene_data.inc", "../../include/hockey.h", "Makefile"]
+
+
+def source_hash():
+    """12-hex sha256 of the library's sources as they are in this tree (== the Makefile's .srchash)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for name in HASH_SOURCES:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:12]
+
+
+def built_hash():
+    """Source hash the in-tree libhockey_hip.so was built from (its .srchash sidecar), or None."""
+    try:
+        with open(LIB_PATH + ".srchash") as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
 
 
 def build(force=False, arch="gfx950"):
@@ -80,12 +105,13 @@ def lib():
     L.hk_observe.argtypes = [vp, vp, vp, vp]
     L.hk_info.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hk_opponent_phase.argtypes = [vp, vp, vp, vp]
+    L.hk_opponent_phase3.argtypes = [vp, vp, vp, vp]
     L.hk_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), vp]
     L.hk_reset_counters.argtypes = [vp, vp]
     L.hk_bytes_per_step.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     for name in ["hk_create", "hk_destroy", "hk_set_policy", "hk_reset", "hk_step", "hk_rollout", "hk_get_state",
                  "hk_set_state",
-                 "hk_observe", "hk_info", "hk_opponent_phase", "hk_counters", "hk_reset_counters", "hk_bytes_per_step"]:
+                 "hk_observe", "hk_info", "hk_opponent_phase", "hk_opponent_phase3", "hk_counters", "hk_reset_counters", "hk_bytes_per_step"]:
         getattr(L, name).restype = i32
     _lib = L
     return L

@@ -272,12 +272,19 @@ class VecHockeyEnv:
         mk = None if mask is None else torch.as_tensor(mask, dtype=torch.uint8, device=self.device).contiguous()
         N.check(self.L.hk_set_state(self._ctx, N.ptr(mk), N.ptr(st), N.ptr(ax), self._stream()), "hk_set_state")
 
-    def opponent_phase(self, new_phase=None):
-        """Return the BasicOpponent phases [N,2] (float64, device); optionally overwrite them."""
-        out = torch.zeros((self.n, 2), dtype=torch.float64, device=self.device)
+    def opponent_phase(self, new_phase=None, rows=2):
+        """Return the BasicOpponent phases [N,rows] (float64, device); optionally overwrite them.  rows=2:
+        player 1 / player 2 (hk_opponent_phase); rows=3 adds player 2's weak bot under a policy2 override
+        (hk_opponent_phase3, include/hockey.h states which step walks which row)."""
+        if rows not in (2, 3):
+            raise ValueError("rows must be 2 or 3")
+        out = torch.zeros((self.n, rows), dtype=torch.float64, device=self.device)
         ph = None if new_phase is None else torch.as_tensor(new_phase, dtype=torch.float64,
                                                             device=self.device).contiguous()
-        N.check(self.L.hk_opponent_phase(self._ctx, N.ptr(out), N.ptr(ph), self._stream()), "hk_opponent_phase")
+        if ph is not None and ph.shape != (self.n, rows):
+            raise ValueError(f"new_phase must have shape ({self.n}, {rows})")
+        fn = self.L.hk_opponent_phase if rows == 2 else self.L.hk_opponent_phase3
+        N.check(fn(self._ctx, N.ptr(out), N.ptr(ph), self._stream()), "hk_opponent_phase")
         return out
 
     def counters(self):

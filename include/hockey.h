@@ -64,7 +64,9 @@ enum {
   HK_CNT_GOALS_P2 = 3,  /* episodes won by player 2 */
   HK_CNT_TOI = 4,       /* solved time-of-impact events */
   HK_CNT_OVERFLOW = 5,  /* island / TOI capacity overflows (must stay 0) */
-  HK_CNT_LARGE_ISLANDS = 6 /* solver calls with more contacts than the register fast path holds */
+  HK_CNT_LARGE_ISLANDS = 6, /* solver calls with more contacts than the register fast path holds */
+  HK_CNT_BAD_POLICY = 7     /* arena-steps whose io.policy2 entry was not an HK_POLICY_* id (that player
+                               acted with zeros); must stay 0 */
 };
 
 typedef struct hk_config {
@@ -105,7 +107,9 @@ typedef struct hk_step_io {
   int32_t flags;          /* HK_STEP_* */
   const uint8_t *policy2; /* [N] u8 per-arena player-2 policy (HK_POLICY_*) for this step, overriding the
                              context's, or NULL: rl/training/opponent_manager.py:62-91 draws player 2's
-                             opponent (self-play / strong / weak bot) per step.  EXTERNAL reads actions[:,4:8].
+                             opponent (self-play / strong / weak bot) per step.  EXTERNAL reads actions[:,4:8],
+                             so io.actions must be given with an override (HK_E_INVALID otherwise); an id
+                             above 3 is counted in HK_CNT_BAD_POLICY and that player acts with zeros.
                              Under an override the strong bot keeps phase row 1 and the weak bot its own row 2
                              (the reference's OpponentManager holds one BasicOpponent of each kind) */
 } hk_step_io;
@@ -144,6 +148,14 @@ int hk_set_state(void *ctx, const uint8_t *mask, const float *state, const int32
 /* BasicOpponent phases ([N,2] f64 device, player 1 / player 2): copied out to phase_out (nullable), then
  * overwritten from phase_in (nullable).  BasicOpponent.__init__ draws U(0, pi) (hockey_env.py:785). */
 int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void *stream);
+
+/* All three phase rows ([N,3] f64 device, same copy-out-then-overwrite contract): row 0 player 1's bot, row 1
+ * player 2's bot under the context policy (and the strong bot under an io.policy2 override), row 2 player 2's
+ * weak bot under an override.  Rule: a step WITH an override walks row 2 for the weak bot and row 1 for the
+ * strong bot; a step WITHOUT one walks row 1 for whichever bot the context policy names.  A caller that mixes
+ * the two on a context whose player-2 policy is weak therefore splits that bot's phase over rows 1 and 2;
+ * the C5 loop (rl/training/opponent_manager.py's mix) passes an override on every step. */
+int hk_opponent_phase3(void *ctx, double *phase_out, const double *phase_in, void *stream);
 
 /* Observation of the current state without stepping ([N,18] f32 each, either may be NULL). */
 int hk_observe(void *ctx, float *obs, float *obs2, void *stream);

@@ -10,6 +10,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
+from hockey_amd._native import built_hash, source_hash  # noqa: E402  (pure Python: no GPU, no library load)
 
 
 def per_launch(counter):
@@ -38,6 +40,7 @@ if __name__ == "__main__":
     d[key] = {"fetch_size_kib_per_launch_raw": fetch_kib, "write_size_kib_per_launch": write_kib,
               "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
               "hbm_bytes_per_launch": read_b + write_b, "launches": [nf, nw], "source": source,
+              "source_hash": source_hash(), "library_hash": built_hash(),
               "note": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (scripts/pmc.sh); "
                       "FETCH_SIZE x2 per MI355X_MICROARCH.md gfx950 correction"}
     json.dump(d, open(out_path, "w"), indent=1)

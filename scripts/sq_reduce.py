@@ -15,6 +15,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
+from hockey_amd._native import built_hash, source_hash  # noqa: E402  (pure Python: no GPU, no library load)
 acc = collections.defaultdict(list)
 for fn in glob.glob(os.path.join(ROOT, "gpurun_out", "sq_*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(fn)):
@@ -45,5 +47,6 @@ if len(sys.argv) > 1 and "SQ_THREAD_CYCLES_VALU" in avg:
     d[key] = {"valu_lane_ops_per_launch": avg["SQ_THREAD_CYCLES_VALU"], "valu_lane_util": lane_util,
               "valu_issue_util": issue_util, "valu_insts_per_wave": avg.get("SQ_INSTS_VALU", 0) / w,
               "waves": w, "counters": avg,
-              "source": sys.argv[2] if len(sys.argv) > 2 else "scripts/sq.sh + scripts/sq_reduce.py"}
+              "source": sys.argv[2] if len(sys.argv) > 2 else "scripts/sq.sh + scripts/sq_reduce.py",
+              "source_hash": source_hash(), "library_hash": built_hash()}
     json.dump(d, open(out_path, "w"), indent=1)

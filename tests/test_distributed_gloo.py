@@ -61,3 +61,43 @@ def test_two_rank_sharding_matches_single_process(tmp_path):
     st, aux = one.get_state()
     assert np.array_equal(st, np.concatenate([r[0]["st"], r[1]["st"]]))
     assert np.array_equal(aux, np.concatenate([r[0]["aux"], r[1]["aux"]]))
+
+
+def _bench(args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=300)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, [json.loads(ln) for ln in lines], p.stderr
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` (no torch.distributed launcher) starts 2 ranks itself; rank 0 prints one line whose
+    n_gpus and whole-job value cover both ranks (CPU rehearsal: gloo, no simulation)."""
+    rc, lines, err = _bench(["--gpus", "2", "--rehearse", "--steps", "4", "--warmup", "1", "--preroll", "0",
+                             "--arenas", "64"])
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["rehearsal"] is True and ln["steps"] == 4
+    assert abs(ln["value"] - 2 * 64 * 4 / (ln["ms_per_step"] * 4 / 1e3)) / ln["value"] < 1e-9
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    rc, lines, err = _bench(["--gpus", "1", "--rehearse", "--steps", "2", "--warmup", "0", "--preroll", "0",
+                             "--arenas", "64"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not lines
+    assert "WORLD_SIZE=2" in err
+
+
+def test_bench_failed_rank_fails_the_launch():
+    """A rank that dies makes the launcher exit non-zero (here: an invalid arena count on every rank)."""
+    rc, lines, err = _bench(["--gpus", "2", "--rehearse", "--steps", "2", "--warmup", "0", "--preroll", "0",
+                             "--arenas", "0"])
+    assert rc != 0

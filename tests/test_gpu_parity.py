@@ -281,20 +281,28 @@ def _res_np(res, t=None):
     return out
 
 
-def _bench_path_lockstep(oracle, n, steps, mode, policies, seed, offset=0, diag_flags=0):
-    """GPU (hk_step for the first half, hk_rollout for the rest) vs the oracle's batched context."""
-    env = _vec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset,
-               diag_flags=diag_flags)
-    ov = oracle.OracleVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
+def _bench_path_lockstep(oracle, n, steps, mode, policies, seed, offset=0, diag_flags=0, keep_mode=True,
+                         vel_ref=False, external=False):
+    """GPU (hk_step for the first half, hk_rollout for the rest) vs the oracle's batched context.  external:
+    U(-1.2, 1.2) joint actions (clipped in both) for the external players."""
+    env = _vec(n, keep=keep_mode, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset,
+               diag_flags=diag_flags, vel_ref_semantics=vel_ref)
+    ov = oracle.OracleVec(n, keep_mode=keep_mode, mode=mode, policies=policies, auto_reset=True, seed=seed,
+                          arena_offset=offset, vel_ref=vel_ref)
+    rng = np.random.default_rng(seed)
+    acts = rng.uniform(-1.2, 1.2, (steps, n, 8)).astype(np.float32) if external else None
     half = steps // 2
     for t in range(half):
-        got = _res_np(env.step(None, with_agent_two=True, record_actions=True, final_obs=True))
-        bad = first_mismatch(t, got, ov.step(with_agent_two=True, final_obs=True))
+        a = None if acts is None else acts[t]
+        got = _res_np(env.step(a, with_agent_two=True, record_actions=True, final_obs=True))
+        bad = first_mismatch(t, got, ov.step(a, with_agent_two=True, final_obs=True))
         if bad:
             return bad
-    ro = env.rollout(steps - half, with_agent_two=True, record_actions=True, final_obs=True)
+    ro = env.rollout(steps - half, actions=None if acts is None else torch.as_tensor(acts[half:], device="cuda:0"),
+                     with_agent_two=True, record_actions=True, final_obs=True)
     for t in range(steps - half):
-        bad = first_mismatch(half + t, _res_np(ro, t), ov.step(with_agent_two=True, final_obs=True))
+        a = None if acts is None else acts[half + t]
+        bad = first_mismatch(half + t, _res_np(ro, t), ov.step(a, with_agent_two=True, final_obs=True))
         if bad:
             return bad
     st, aux = env.get_state()
@@ -305,6 +313,29 @@ def _bench_path_lockstep(oracle, n, steps, mode, policies, seed, offset=0, diag_
     assert np.array_equal(c[:5], oc[:5]), (c[:7], oc[:7])
     env.close()
     return {"counters": c}
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_keep_mode_false_with_physics_lockstep_vs_oracle(oracle, mode):
+    """Hockey-v0 with keep_mode=False (hockey_env.py:91): player 2's action at index 3 (:663), no hold / shoot
+    (:668-680), world.Step running -- external random actions against the fused BasicOpponent(keep_mode=False),
+    then bot vs bot, bit-exact through hk_step and hk_rollout in every mode."""
+    out = _bench_path_lockstep(oracle, 128, 300, mode, ("external", "strong"), seed=60 + mode, keep_mode=False,
+                               external=True)
+    assert "field" not in out, out
+    out = _bench_path_lockstep(oracle, 128, 300, mode, ("weak", "strong"), seed=63 + mode, keep_mode=False)
+    assert "field" not in out, out
+    assert out["counters"][N.CNT_EPISODES] > 0
+
+
+def test_live_velocity_semantics_with_physics_lockstep_vs_oracle(oracle):
+    """vel_ref_semantics=1 (live-reference velocity getters in _check_boundaries,
+    hockey_env.py:425-432) with world.Step running, bit-exact against the oracle."""
+    out = _bench_path_lockstep(oracle, 128, 300, 0, ("external", "external"), seed=66, vel_ref=True, external=True)
+    assert "field" not in out, out
+    out = _bench_path_lockstep(oracle, 256, 400, 0, ("strong", "strong"), seed=67, vel_ref=True)
+    assert "field" not in out, out
+    assert out["counters"][N.CNT_TOI] > 0
 
 
 @pytest.mark.parametrize("mode,steps", [(0, 600), (1, 300), (2, 300)])
@@ -384,7 +415,7 @@ def test_autoreset_external_policy_transitions(oracle):
 def test_c4_shard_131072_arenas(oracle):
     """BASELINE C4's per-GPU shard: 131 072 arenas (random vs random, auto-reset).  Checks: counters and
     finiteness at full size, 1 x 131 072 == 2 x 65 536 shard contexts with global offsets bit for bit, and
-    three 256-arena blocks (start, middle, end) equal to the oracle run with the same global ids."""
+    three 256-arena blocks (start, middle, end) equal, at every step, to the oracle run with the same global ids."""
     n, steps, seed = 131072, 300, 2024
     full = _vec(n, policies=("random", "random"), auto_reset=True, seed=seed, arena_offset=n)  # rank 1 of C4
     halves = [_vec(n // 2, policies=("random", "random"), auto_reset=True, seed=seed, arena_offset=n + k * n // 2)
@@ -396,14 +427,12 @@ def test_c4_shard_131072_arenas(oracle):
         res = full.step(None, with_agent_two=True, final_obs=True)
         for h in halves:
             h.step(None)
-        if t % 25 == 0 or t == steps - 1:  # sampled per-step outputs of the three blocks
-            got = _res_np(res)
-        for b, ov in zip(blocks, ovs):
+        for b, ov in zip(blocks, ovs):  # every step's outputs of the three blocks (sliced on the device)
             want = ov.step(with_agent_two=True, final_obs=True)
-            if t % 25 == 0 or t == steps - 1:
-                sl = {k: v[b:b + 256] for k, v in got.items()}
-                bad = first_mismatch(t, sl, want)
-                assert bad is None, (b, bad)
+            sl = {f: _np(getattr(res, f)[b:b + 256]) for f in ("obs", "obs2", "reward", "reward2", "done", "info",
+                                                                  "info2", "final_obs")}
+            bad = first_mismatch(t, sl, want, fields=tuple(sl))
+            assert bad is None, (b, bad)
     torch.cuda.synchronize()
     st, aux = full.get_state()
     st, aux = _np(st), _np(aux)
@@ -422,3 +451,32 @@ def test_c4_shard_131072_arenas(oracle):
     assert np.array_equal(c[:7], ch[:7])
     for e in [full, *halves]:
         e.close()
+
+
+def test_policy2_validation_and_phase_rows():
+    """hk_step rejects a policy2 override without io.actions (an override may pick EXTERNAL); an id that is
+    not an HK_POLICY_* is counted in HK_CNT_BAD_POLICY and that player acts with zeros, never as a bot; and
+    hk_opponent_phase3 reads / writes all three phase rows ([N,3])."""
+    n = 128
+    env = _vec(n, policies=("strong", "strong"), auto_reset=True, seed=5)
+    p2 = torch.full((n,), 2, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(N.HockeyNativeError, match="policy2"):
+        env.step(None, policy2=p2)
+    ph = torch.rand((n, 3), dtype=torch.float64, device="cuda:0") * 3
+    env.opponent_phase(ph, rows=3)
+    assert torch.equal(env.opponent_phase(rows=3), ph)
+    assert torch.equal(env.opponent_phase(), ph[:, :2])
+    acts = torch.zeros((n, 8), device="cuda:0")
+    p2[: n // 2] = 7  # invalid ids
+    env.reset_counters()
+    res = env.step(acts, policy2=p2, record_actions=True)
+    a = _np(res.actions)
+    assert np.all(a[: n // 2, 4:8] == 0)  # zeros, not a bot
+    assert np.any(a[n // 2:, 4:8] != 0)   # the weak bot acts where the id is valid
+    c = env.counters()
+    assert c[N.CNT_BAD_POLICY] == n // 2 and c[N.CNT_STEPS] == n
+    ph2 = _np(env.opponent_phase(rows=3))
+    ph0 = _np(ph)
+    assert np.array_equal(ph2[: n // 2, 1:], ph0[: n // 2, 1:])  # no bot walked player 2's rows there
+    assert np.all(ph2[n // 2:, 2] != ph0[n // 2:, 2]) and np.array_equal(ph2[n // 2:, 1], ph0[n // 2:, 1])
+    env.close()

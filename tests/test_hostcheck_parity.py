@@ -94,12 +94,15 @@ def test_fused_opponents_autoreset_run(oracle):
 from vec_lockstep import first_mismatch  # noqa: E402
 
 
-def _vec_lockstep(oracle, n, steps, mode, policies, seed, external=False, offset=0, mix=False):
+def _vec_lockstep(oracle, n, steps, mode, policies, seed, external=False, offset=0, mix=False, keep_mode=True,
+                  vel_ref=False):
     """The kernel source (host build) vs the oracle's batched context on the hk_step contract: fused
     policies with Philox increments (opp_inc NULL), device auto-reset with episode counters.  mix: player 2's
     policy is drawn per arena and step from {external, weak, strong} (hk_step_io.policy2)."""
-    env = HostVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
-    ov = oracle.OracleVec(n, mode=mode, policies=policies, auto_reset=True, seed=seed, arena_offset=offset)
+    env = HostVec(n, keep_mode=keep_mode, mode=mode, policies=policies, auto_reset=True, seed=seed,
+                  arena_offset=offset, vel_ref=vel_ref)
+    ov = oracle.OracleVec(n, keep_mode=keep_mode, mode=mode, policies=policies, auto_reset=True, seed=seed,
+                          arena_offset=offset, vel_ref=vel_ref)
     rng = np.random.default_rng(seed)
     for t in range(steps):
         acts = rng.uniform(-1.2, 1.2, (n, 8)).astype(np.float32) if external else None
@@ -151,3 +154,24 @@ def test_island_retirement_and_slot_swaps_vs_oracle(oracle):
     assert "field" not in out, out
     d = velocity_diag()
     assert d[0] > 0 and d[1] > 0, d
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_keep_mode_false_with_physics_vs_oracle_vec(oracle, mode):
+    """Hockey-v0 with keep_mode=False (hockey_env.py:91): 6-dim joint action, player 2's action at index 3
+    (:663), no hold / shoot (:668-680) -- with world.Step running, external random actions and the fused
+    BasicOpponent(keep_mode=False) in every mode."""
+    out = _vec_lockstep(oracle, 48, 260, mode, ("external", "strong"), seed=41 + mode, external=True,
+                        keep_mode=False)
+    assert "field" not in out, out
+    out = _vec_lockstep(oracle, 48, 200, mode, ("weak", "strong"), seed=44 + mode, keep_mode=False)
+    assert "field" not in out, out
+
+
+def test_live_velocity_semantics_with_physics_vs_oracle_vec(oracle):
+    """SURVEY App. B Q1 live-reference velocity getters (vel_ref_semantics=1, hockey_env.py:425-432) with
+    world.Step running: random external actions (boundary hits) and the strong-vs-strong workload."""
+    out = _vec_lockstep(oracle, 48, 300, 0, ("external", "external"), seed=47, external=True, vel_ref=True)
+    assert "field" not in out, out
+    out = _vec_lockstep(oracle, 48, 300, 1, ("strong", "strong"), seed=48, vel_ref=True)
+    assert "field" not in out, out

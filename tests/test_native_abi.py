@@ -12,7 +12,7 @@ from conftest import ROOT
 def _declared():
     src = open(os.path.join(ROOT, "include", "hockey.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(hk_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(hk_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_boundary():
@@ -78,3 +78,25 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 text = open(os.path.join(dirpath, f), errors="replace").read()
                 assert "hk_oracle" not in text and "import oracle" not in text, f
+
+
+def test_source_hash_matches_makefile_recipe():
+    """bench.py's counter provenance: hockey_amd._native.source_hash() hashes exactly the Makefile's HASHSRC
+    list (SRC, HDR, Makefile) in its order, so it equals the .srchash sidecar make writes next to the library."""
+    import hashlib
+    import subprocess
+
+    from hockey_amd import _native as N
+
+    mk = open(os.path.join(N.CSRC, "Makefile")).read()
+
+    def var(name):
+        return re.search(rf"^{name} = (.*)$", mk, flags=re.M).group(1).split()
+
+    assert re.search(r"^HASHSRC = \$\(SRC\) \$\(HDR\) Makefile$", mk, flags=re.M)
+    assert var("SRC") + var("HDR") + ["Makefile"] == N.HASH_SOURCES
+    cat = b"".join(open(os.path.join(N.CSRC, f), "rb").read() for f in N.HASH_SOURCES)
+    assert N.source_hash() == hashlib.sha256(cat).hexdigest()[:12]
+    out = subprocess.check_output(f"cat {' '.join(N.HASH_SOURCES)} | sha256sum | cut -c1-12", shell=True,
+                                  cwd=N.CSRC, text=True).strip()
+    assert out == N.source_hash()

@@ -9,13 +9,18 @@ import numpy as np
 FIELDS = ("obs", "obs2", "reward", "reward2", "done", "info", "info2", "actions", "final_obs")
 
 
-def first_mismatch(step, got, want, fields=FIELDS):
-    """Return a description of the first differing field / arena, or None."""
-    for f in fields:
+def first_mismatch(step, got, want, fields=None):
+    """Return a description of the first differing field / arena, or None.
+
+    fields: the fields to compare (default: every field the oracle produced).  A requested field that either
+    side lacks is itself a mismatch, so an output the implementation silently dropped cannot pass."""
+    for f in (tuple(want) if fields is None else fields):
         if f not in want or got.get(f) is None:
-            continue
+            return {"step": step, "field": f, "missing": "oracle" if f not in want else "implementation"}
         g = np.asarray(got[f]).reshape(want[f].shape[0], -1)
         w = want[f].reshape(want[f].shape[0], -1)
+        if g.shape != w.shape or g.dtype.itemsize != w.dtype.itemsize:
+            return {"step": step, "field": f, "shape": [g.shape, w.shape], "dtype": [str(g.dtype), str(w.dtype)]}
         ok = np.all(g.view(np.uint8) == w.view(np.uint8), axis=1) if g.dtype == np.uint8 else \
             np.all(g.view(np.uint32) == w.view(np.uint32), axis=1)
         if not ok.all():
