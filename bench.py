@@ -271,28 +271,31 @@ def time_facade(steps, dev):
                       "reset(seed) on done: per step one hk_step launch + obs/reward/done/info copies to the host"}
 
 
-def time_c5(n, steps, dev):
-    """BASELINE C5: one round of the batched TD3 loop (hockey_amd.td3.train): actor forward, per-arena per-step
-    opponent mix (strong / weak bot fused in the kernel, self-play snapshot), hk_step, replay push; the
-    round's single learner update is excluded by timing a warm round against a round of the same shape."""
-    import torch
-
-    from hockey_amd.td3 import TD3Config, train
+def time_c5(n, steps, dev, batch=16384):
+    """BASELINE C5: one round of the batched TD3 loop (hockey_amd.td3.train) on n arenas: device reset, actor
+    forward + exploration noise, per-arena per-step opponent mix (strong / weak bot fused in the kernel,
+    self-play snapshot forward), hk_step, replay push -- then the learner updates of that round at the
+    reference's replay ratio (32 updates x 256 samples per 500-step episode = 16.4 samples per transition,
+    rl/training/train.py:145-207) as graph-captured updates of `batch` samples.  Reports the whole round
+    (collection + updates) and the collection alone; round 2 is timed (the self-play pool is populated)."""
+    from hockey_amd.td3 import TD3Config, train, updates_for
 
     cfg = TD3Config(max_steps=steps, start_steps=0)
     table = [(1.0, 0.35, 0.35, 0.30)]  # stage-3's last curriculum row (self-play active from round 2)
-    train(n_arenas=n, rounds=2, cfg=TD3Config(max_steps=5, start_steps=0), device=dev, updates_per_round=1,
-          curriculum=table, self_play_interval=n, reset="device")  # warm-up (kernels, allocator)
-    torch.cuda.synchronize()
-    marks = []
-    agent, st = train(n_arenas=n, rounds=2, cfg=cfg, device=dev, updates_per_round=1, curriculum=table,
-                      self_play_interval=n, reset="device",
-                      log=lambda r, s: (torch.cuda.synchronize(), marks.append(time.perf_counter())))
-    sec = marks[1] - marks[0]  # round 2: the snapshot pool is populated, so the mix includes self-play
-    return {"value": n * steps / sec, "unit": "env-steps/s", "arenas": n, "steps": steps,
+    train(n_arenas=n, rounds=2, cfg=TD3Config(max_steps=5, start_steps=0), device=dev, curriculum=table,
+          self_play_interval=n, reset="device", learner_batch=batch)  # warm-up (kernels, graph, allocator)
+    agent, st = train(n_arenas=n, rounds=2, cfg=cfg, device=dev, curriculum=table, self_play_interval=n,
+                      reset="device", learner_batch=batch, timing=True)
+    collect, update = st["round_time"][1]
+    ups = updates_for(cfg, n, steps, batch)
+    return {"value": n * steps / (collect + update), "unit": "env-steps/s", "arenas": n, "steps": steps,
+            "collect_value": n * steps / collect, "collect_s": collect, "update_s": update,
+            "updates": ups, "batch": batch, "samples_per_transition": ups * batch / (n * steps),
             "opponents": st["opponents"][1],
-            "sample": f"round 2 of hockey_amd.td3.train on {n} arenas x {steps} steps: device reset, actor + noise, "
-                      "opponent mix (strong / weak bot / self-play snapshot), hk_step, replay push, 1 learner update"}
+            "sample": f"round 2 of hockey_amd.td3.train on {n} arenas x {steps} steps (device reset, actor + noise, "
+                      f"opponent mix, hk_step, replay push) + {ups} learner updates of {batch} samples "
+                      f"(the reference's 16.4 samples per stored transition); value = whole round, "
+                      f"collect_value = collection only"}
 
 
 def time_c4(n, steps, preroll_steps, seed, dev):

@@ -20,7 +20,8 @@ Batched differences (by design, documented): the draws come from a torch generat
 the process-global ``np.random``; the snapshot is sampled once per step for all arenas (the reference samples
 one per step for its single env); ``register_outcome`` counts the done steps of self-play arenas against the
 snapshot they faced (the reference charges the last sampled snapshot for every done step of any opponent),
-accumulated on the device and folded into the scores once per round.
+tallied per step on the device and folded into the scores step by step at the end of the round (within one
+step, the non-win outcomes are applied before the wins; clipping follows every outcome as in the reference).
 """
 import copy
 import math
@@ -70,9 +71,16 @@ class SelfPlayPool:
             self.scores.pop(0)
 
     def update_difficulty(self, idx, wins, others):
-        """`others` outcomes that are not agent wins (x1.2 each) and `wins` agent wins (x0.95 each), clipped."""
-        s = math.log(self.scores[idx]) + others * math.log(SCORE_LOSS) + wins * math.log(SCORE_WIN)
-        self.scores[idx] = float(np.clip(math.exp(min(s, 50.0)), SCORE_MIN, SCORE_MAX))
+        """One step's outcomes against snapshot ``idx``: ``others`` outcomes that are not agent wins (x1.2 each)
+        then ``wins`` agent wins (x0.95 each), clipped to [0.1, 10] after EVERY outcome as the reference does
+        (self_play.py:45-55).  Both runs are monotone, so clipping after each factor equals clipping the run's
+        product once: min(10, s * 1.2^others), then max(0.1, s * 0.95^wins)."""
+        s = self.scores[idx]
+        if others:
+            s = min(SCORE_MAX, math.exp(min(math.log(s) + others * math.log(SCORE_LOSS), 50.0)))
+        if wins:
+            s = max(SCORE_MIN, math.exp(math.log(s) + wins * math.log(SCORE_WIN)))
+        self.scores[idx] = float(np.clip(s, SCORE_MIN, SCORE_MAX))
 
     def sample(self):
         """Score-weighted snapshot index (get_opponent), or None with an empty pool."""
@@ -111,7 +119,7 @@ class OpponentMix:
 
     def reset_stats(self):
         self._counts = torch.zeros(3, dtype=torch.int64, device=self.device)  # strong, weak, self-play
-        self._outcomes = {}  # snapshot index -> device tensor [wins, others]
+        self._outcomes = []  # per step: device tensor [snapshot index, wins, others]
 
     def select(self, obs2):
         """(policy2 [N] uint8, player-2 actions [N,4] or None, snapshot index or None) for this step.
@@ -138,23 +146,24 @@ class OpponentMix:
 
     def register_outcomes(self, done, reward):
         """Done steps of this step's self-play arenas: agent win (reward > 0) or not (opponent_manager
-        register_outcome -> update_difficulty).  Accumulated on the device; folded in by end_round()."""
+        register_outcome -> update_difficulty).  Tallied per step on the device; end_round() applies the steps in
+        order, clipping after every outcome."""
         if self._idx is None:
             return
         d = (done != 0) & self._sp_mask
         win = d & (reward > 0)
-        acc = self._outcomes.setdefault(self._idx, torch.zeros(2, dtype=torch.int64, device=self.device))
-        acc += torch.stack([win.sum(), (d & ~win).sum()])
+        self._outcomes.append(torch.stack([torch.full((), self._idx, dtype=torch.int64, device=self.device),
+                                           win.sum(), (d & ~win).sum()]))
 
     def end_round(self, actor=None, episodes=0):
         """Fold the round's outcomes into the snapshot scores, advance the self-play episode counter (taking a
         snapshot on an interval boundary) and return the round's opponent counts."""
         counts = self._counts.cpu().tolist()
         if self.pool is not None:
-            for idx, acc in self._outcomes.items():
-                if idx < len(self.pool):
-                    w, o = acc.cpu().tolist()
-                    self.pool.update_difficulty(idx, w, o)
+            if self._outcomes:
+                for idx, w, o in torch.stack(self._outcomes).cpu().tolist():
+                    if idx < len(self.pool) and (w or o):
+                        self.pool.update_difficulty(idx, w, o)
             if actor is not None and episodes:
                 self.pool.step(actor, episodes)
         self.reset_stats()

@@ -80,3 +80,51 @@ def test_per_step_draw_probabilities():
     counts = mix.end_round()
     assert math.isclose(mix.pool.scores[0], 0.95 * 1.2 * 1.2)
     assert counts["self_play"] == int(sp.sum()) and sum(counts.values()) == 2 * n
+
+
+def _ref_update_difficulty(score, win):
+    """rl/training/self_play.py:45-55, one outcome at a time (restated)."""
+    score = score * 1.2 if win == 0 else score * 0.95
+    return float(np.clip(score, 0.1, 10.0))
+
+
+def test_difficulty_clips_after_every_outcome_like_the_reference():
+    """Saturation: 20 non-wins then 30 wins -> 10 * 0.95^30 = 2.146 in the reference (clipped at 10 on the way
+    up), not 1.2^20 * 0.95^30 = 8.2; the per-step tallies reproduce any outcome sequence whose steps hold
+    their non-wins before their wins."""
+    pool = SelfPlayPool(interval=1, pool_size=1, seed=0)
+    pool.add_snapshot(Actor())
+    pool.update_difficulty(0, wins=0, others=20)
+    pool.update_difficulty(0, wins=30, others=0)
+    assert math.isclose(pool.scores[0], 10 * 0.95 ** 30)
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        pool.scores = [float(rng.uniform(0.1, 10))]
+        ref = pool.scores[0]
+        for _ in range(40):  # steps
+            w, o = (int(x) for x in rng.integers(0, 25, 2))
+            for win in [0] * o + [1] * w:
+                ref = _ref_update_difficulty(ref, win)
+            pool.update_difficulty(0, wins=w, others=o)
+            assert math.isclose(pool.scores[0], ref, rel_tol=1e-9), (pool.scores[0], ref)
+
+
+def test_round_outcomes_fold_step_by_step():
+    n = 64
+    mix = OpponentMix(n, [(1.0, 0.0, 0.0, 1.0)], device="cpu", seed=2)
+    mix.pool.add_snapshot(Actor())
+    ref = 1.0
+    for t in range(30):
+        mix.select(torch.zeros(n, 18))
+        done = torch.zeros(n, dtype=torch.uint8)
+        reward = torch.zeros(n)
+        k = 8 if t < 10 else 3  # many non-wins early (saturate at 10), wins later
+        done[:k] = 1
+        if t >= 10:
+            reward[:2] = 10.0
+        mix.register_outcomes(done, reward)
+        wins = int(((done != 0) & (reward > 0)).sum())
+        for win in [0] * (k - wins) + [1] * wins:
+            ref = _ref_update_difficulty(ref, win)
+    mix.end_round()
+    assert math.isclose(mix.pool.scores[0], ref, rel_tol=1e-9)

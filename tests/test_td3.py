@@ -1,12 +1,19 @@
 """§8 row f3: the GPU-resident TD3 (hockey_amd/td3.py).  CPU tests pin the learner arithmetic against the
 reference formulas (rl/td3/learner.py:55-218, rl/utils/torch_utils.py:12-24); the GPU test runs the batched
 collection + update loop over real arenas."""
+import math
+
 import numpy as np
 import pytest
 import torch
 
+import os
+
 from hockey_amd.evaluate import load_actor
-from hockey_amd.td3 import TD3, ReplayRing, TD3Config, smooth_l1
+from hockey_amd.noise import GaussianNoise, OrnsteinUhlenbeckNoise, PinkNoise, UniformNoise, make_noise
+from hockey_amd.td3 import TD3, Learner, PrioritizedRing, ReplayRing, TD3Config, smooth_l1, updates_for
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def test_smooth_l1_matches_reference_formula():
@@ -55,8 +62,156 @@ def test_replay_ring_wraps():
     for k in range(3):
         ring.push(torch.full((4, 18), float(k)), torch.zeros(4, 4), torch.zeros(4), torch.zeros(4, 18),
                   torch.zeros(4))
-    assert len(ring) == 10 and ring.pos == 2
+    assert len(ring) == 10 and ring.pos == 2 and float(ring.size_t) == 10
     assert ring.s[0, 0] == 2 and ring.s[9, 0] == 2 and ring.s[7, 0] == 1
+    i = ring.sample_indices(10_000)
+    assert int(i.min()) == 0 and int(i.max()) == 9  # (rand * size).astype(int) over the filled slots
+
+
+class _RefPER:
+    """rl/replay/prioritized_buffer.py:6-69 weight bookkeeping, restated with numpy (one push at a time)."""
+
+    def __init__(self, cap, init_weight=1e8):
+        self.cap, self.size, self.cur = cap, 0, 0
+        self.weights = np.full(cap, init_weight, np.float32)
+
+    def push(self):
+        self.size = min(self.size + 1, self.cap)
+        self.cur = (self.cur + 1) % self.cap
+        self.weights[self.cur - 1] = np.max(self.weights[: self.size])
+
+    def probs(self):
+        w = np.maximum(np.nan_to_num(self.weights[: self.size], nan=0.0, posinf=0.0, neginf=0.0), 1e-6)
+        return w / w.sum()
+
+
+def test_prioritized_ring_matches_reference_bookkeeping():
+    cap = 50
+    ring, ref = PrioritizedRing(cap, device="cpu", beta=0.15), _RefPER(cap)
+    rng = np.random.default_rng(0)
+    for k in range(9):
+        n = int(rng.integers(1, 17))
+        ring.push(torch.randn(n, 18), torch.randn(n, 4), torch.randn(n), torch.randn(n, 18), torch.zeros(n))
+        for _ in range(n):
+            ref.push()
+        assert np.array_equal(ring.w.numpy(), ref.weights), k
+        # sample, then the sampled slots take their TD-error priorities (learner.update_critic)
+        s, a, r, s2, d, iw = ring.sample(8)
+        inds = ring.last.numpy()
+        assert inds.max() < ref.size
+        p_b = ref.weights[inds] / ref.weights[inds].sum()  # learner._compute_importance_weights
+        w = (1 / (p_b * ref.size)) ** 0.15
+        assert np.allclose(iw.numpy(), w / w.max(), rtol=1e-5)
+        td = torch.rand(8) * 3
+        ring.update_priorities(td)
+        ref.weights[inds] = np.clip(td.numpy(), 1e-6, 1e6)
+        assert np.array_equal(ring.w.numpy(), ref.weights)
+    # sampling follows P(i) = w_i / sum(w) over the filled slots
+    ring.w[:] = 1.0
+    ring.w[3] = 40.0
+    hits = torch.cat([ring.sample_indices(4096) for _ in range(8)])
+    p = ring.w[:ring.size].double() / ring.w[:ring.size].double().sum()
+    assert abs(float((hits == 3).double().mean()) - float(p[3])) < 0.02
+    assert int(hits.max()) < ring.size
+
+
+def test_weighted_smooth_l1():
+    x, y, w = torch.tensor([0.0, 0.5, 3.0, -2.0]), torch.tensor([0.2, 0.0, 0.0, 0.0]), torch.tensor([1., 2., 3., 4.])
+    d = x - y
+    ref = torch.where(d.abs() < 1, 0.5 * w * d ** 2, (d.abs() - 0.5) * w).mean()
+    assert torch.equal(smooth_l1(x, y, w), ref)
+
+
+def test_noise_processes_match_reference_formulas():
+    n, dim = 4096, 4
+    g = GaussianNoise(n, dim, 0.2, "cpu", 0)
+    x = g()
+    assert x.shape == (n, dim) and abs(float(x.std()) - 0.2) < 0.01
+    u = make_noise("uniform", n, dim, 0.2, 500, "cpu", 0)
+    x = u()
+    assert float(x.abs().max()) <= 0.2 * np.sqrt(3) and abs(float(x.std()) - 0.2) < 0.01
+    # OU: x <- x + theta (mu - x) dt + sigma sqrt(dt) N(0,1), dt = 1.0 as the agent builds it, reset to 0
+    ou = make_noise("ornstein-uhlenbeck", 3, dim, 0.2, 500, "cpu", 7)
+    assert isinstance(ou, OrnsteinUhlenbeckNoise) and ou.dt == 1.0 and ou.theta == 0.15
+    twin = torch.Generator()
+    twin.manual_seed(7 + 0xA0)
+    xr = torch.zeros(3, dim)
+    for _ in range(5):
+        xr = xr + 0.15 * (0.0 - xr) * 1.0 + 0.2 * 1.0 * torch.randn((3, dim), generator=twin)
+        assert torch.allclose(ou(), xr)
+    ou.reset()
+    assert torch.equal(ou.x, torch.zeros(3, dim))
+    # pink: unit-variance blocks of seq_len steps with a 1/f power spectrum, renewed when used up
+    pk = make_noise("pink", 512, dim, 0.3, 256, "cpu", 1)
+    assert isinstance(pk, PinkNoise)
+    blk = pk.block
+    assert blk.shape == (512, dim, 256)
+    assert torch.allclose(blk.std(dim=-1, unbiased=False), torch.ones(512, dim, dtype=blk.dtype), atol=1e-9)
+    psd = (torch.fft.rfft(blk, dim=-1).abs() ** 2).mean(dim=(0, 1))
+    f = torch.fft.rfftfreq(256, dtype=torch.float64)
+    slope = np.polyfit(np.log(f[2:100].numpy()), np.log(psd[2:100].numpy()), 1)[0]
+    assert -1.25 < slope < -0.75  # power ~ 1/f
+    first = pk()
+    assert torch.allclose(first, (0.3 * blk[:, :, 0]).float())
+    for _ in range(255):
+        pk()
+    pk()  # the 257th draw starts a new block
+    assert pk.idx == 1 and not torch.equal(pk.block, blk)
+    assert isinstance(make_noise("gaussian", 1, 4, 0.2, 10, "cpu"), GaussianNoise)
+    assert isinstance(make_noise("uniform", 1, 4, 0.2, 10, "cpu"), UniformNoise)
+    with pytest.raises(ValueError):
+        make_noise("brown", 1, 4, 0.2, 10, "cpu")
+
+
+def test_noise_schedule_and_random_phase():
+    cfg = TD3Config(start_steps=10, use_noise_annealing=True, noise_anneal_mode="linear", noise_min_scale=0.07)
+    agent = TD3(cfg, device="cpu", max_total_steps=100, n_envs=4)
+    agent.total_steps = 50
+    assert math.isclose(agent.noise_scale(), 0.1)
+    agent.total_steps = 99
+    assert agent.noise_scale() == 0.07
+    agent.cfg.noise_anneal_mode = "exp"
+    agent.total_steps = 20
+    assert math.isclose(agent.noise_scale(), 0.2 * 0.1 ** 0.2)
+    agent.cfg.use_noise_annealing = False
+    assert agent.noise_scale() == 0.2
+    # get_action: arena i of a batch is call total_steps + i + 1; random while that is below start_steps
+    agent = TD3(TD3Config(start_steps=10, action_noise_scale=1e-12), device="cpu", n_envs=4)
+    obs = torch.zeros(4, 18)
+    agent.act(obs)  # calls 1..4: random
+    a = agent.act(obs)  # calls 5..8: random
+    assert agent.total_steps == 8
+    a = agent.act(obs)  # calls 9..12: 9 random, 10..12 the (noise-free) actor
+    pol = agent.actor(obs)
+    assert not torch.allclose(a[0], pol[0]) and torch.allclose(a[1:], pol[1:])
+    assert torch.equal(agent.act(obs, noise=False), pol) and agent.total_steps == 12
+
+
+def test_stage1_config_and_replay_ratio():
+    cfg = TD3Config.from_json(os.path.join(GOLDEN, "stage1_config.json"))
+    assert (cfg.buffer_size, cfg.noise_min_scale, cfg.use_self_play, cfg.prioritized_replay) == (100_000, 0.1, False,
+                                                                                                  False)
+    assert math.isclose(cfg.replay_ratio, 32 * 256 / 500)
+    assert updates_for(cfg, 1, 500) == 32  # train_iters per 500-step episode at the reference's batch
+    assert updates_for(cfg, 20, 500) == 640
+    assert updates_for(cfg, 65536, 50, batch=16384) == round(16.384 * 65536 * 50 / 16384)
+
+
+def test_learner_eager_updates_on_cpu():
+    torch.manual_seed(0)
+    agent = TD3(TD3Config(batch_size=16), device="cpu")
+    for ring in (ReplayRing(64, device="cpu"), PrioritizedRing(64, device="cpu")):
+        ring.push(torch.randn(40, 18), torch.rand(40, 4) * 2 - 1, torch.randn(40), torch.randn(40, 18),
+                  (torch.rand(40) < 0.2).float())
+        lr = Learner(agent, ring, 16, graphs=True)  # no GPU: eager
+        before = [p.clone() for p in agent.actor.parameters()]
+        t0 = agent.train_step
+        lr.run(5)
+        assert agent.train_step == t0 + 5
+        cl, al = lr.take_losses()
+        assert np.isfinite(cl) and np.isfinite(al)
+        assert any(not torch.equal(b, p) for b, p in zip(before, agent.actor.parameters()))
+    assert float(ring.w[:40].max()) < 1e8  # sampled priorities were updated
 
 
 @pytest.mark.gpu
@@ -65,26 +220,70 @@ def test_batched_training_loop_runs():
 
     cfg = TD3Config(max_steps=60, start_steps=256, batch_size=128)
     agent, st = train(n_arenas=256, rounds=3, cfg=cfg, updates_per_round=20, seed=3)
-    assert st["env_steps"] == 3 * 60 * 256 and st["updates"] == 60
-    assert all(torch.isfinite(torch.tensor(st["critic_loss"]))) and len(st["actor_loss"]) == 30
+    assert st["env_steps"] == 3 * 60 * 256 and st["updates"] == 60 and agent.train_step == 60
+    assert all(np.isfinite(st["critic_loss"])) and len(st["actor_loss"]) == 3
     x = torch.zeros(4, 18, device="cuda:0")
     assert torch.isfinite(agent.actor(x)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("noise,per", [("ornstein-uhlenbeck", True), ("pink", False), ("uniform", True)])
+def test_learner_options_on_gpu(noise, per):
+    """The reference's learner options (rl/td3/agent.py:128-156 noise kinds, rl/replay/prioritized_buffer.py)
+    through the batched loop: updates run (graph-captured pairs), priorities move off their initial 1e8."""
+    from hockey_amd.td3 import train
+
+    cfg = TD3Config(max_steps=40, start_steps=0, batch_size=256, noise_mode=noise, prioritized_replay=per,
+                    use_self_play=False, curriculum_name="stage1")
+    agent, st = train(n_arenas=128, rounds=3, cfg=cfg, seed=4)
+    assert st["updates"] == 3 * updates_for(cfg, 128, 40)
+    assert all(np.isfinite(st["critic_loss"])) and all(np.isfinite(st["actor_loss"]))
+    assert st["opponents"][0]["weak"] == 40 * 128  # stage-1 curriculum: weak bot only
+
+
+@pytest.mark.gpu
+def test_graph_captured_updates_equal_eager_updates():
+    """Learner: the HIP-graph replay of an update pair performs the same arithmetic as the eager updates.  With
+    identical ring entries (sampling cannot matter) and no target smoothing noise, both paths are
+    deterministic, so the parameters after 40 updates agree."""
+    dev = "cuda:0"
+    nets = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        cfg = TD3Config(batch_size=64, target_action_noise_scale=0.0)
+        agent = TD3(cfg, device=dev, seed=0)
+        ring = ReplayRing(512, device=dev)
+        g = torch.Generator().manual_seed(1)
+        one = [torch.randn(1, 18, generator=g), torch.rand(1, 4, generator=g) * 2 - 1, torch.randn(1, generator=g),
+               torch.randn(1, 18, generator=g), torch.zeros(1)]
+        ring.push(*(t.expand(512, *t.shape[1:]).contiguous().to(dev) for t in one))
+        lr = Learner(agent, ring, 64, graphs=graphs, warm_pairs=2)
+        for _ in range(4):
+            lr.run(10)
+        assert agent.train_step == 40
+        assert (lr.graph is not None) == graphs
+        nets.append(torch.cat([p.detach().flatten() for p in list(agent.actor.parameters()) +
+                               list(agent.critic.parameters()) + list(agent.target_actor.parameters())]))
+    assert torch.allclose(nets[0], nets[1], rtol=1e-5, atol=1e-6), (nets[0] - nets[1]).abs().max()
 
 
 @pytest.mark.gpu
 def test_c5_training_loop_65536_arenas_with_opponent_mix():
     """BASELINE C5: the TD3 loop fed by 65 536 GPU arenas, player 2 re-drawn per arena and step between the
     strong bot, the weak bot and a self-play snapshot (rl/training/opponent_manager.py:62-91); the pool
-    snapshots the actor every 65 536 episodes, i.e. after every round here."""
+    snapshots the actor every 65 536 episodes, i.e. after every round here.  The ring holds a whole round of
+    every arena; the updates run at the reference's replay ratio with a large batch."""
     from hockey_amd.td3 import train
 
     n, rounds, steps = 65536, 3, 40
     cfg = TD3Config(max_steps=steps, start_steps=0, batch_size=256)
-    agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, updates_per_round=10, seed=5,
+    agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, seed=5, learner_batch=16384,
                       curriculum=[(1.0, 0.35, 0.35, 0.30)], self_play_interval=n, pool_size=2)
     assert st["env_steps"] == rounds * steps * n
-    assert st["replay_size"] == min(cfg.buffer_size, n * steps * 4)
-    assert st["updates"] == rounds * 10 and len(st["actor_loss"]) == rounds * 5
+    assert st["replay_capacity"] == n * steps and st["replay_size"] == n * steps
+    ups = updates_for(cfg, n, steps, batch=16384)
+    assert ups == round(16.384 * n * steps / 16384) and st["updates"] == rounds * ups
+    assert abs(st["replay_ratio"] - 16.384) < 0.01
     assert all(np.isfinite(st["critic_loss"])) and all(np.isfinite(st["actor_loss"]))
     assert st["pool_size"] == [1, 2, 2]  # one snapshot per round, capped at pool_size
     first, *later = st["opponents"]
