@@ -278,16 +278,17 @@ def time_c5(n, steps, dev, batch=16384):
     reference's replay ratio (32 updates x 256 samples per 500-step episode = 16.4 samples per transition,
     rl/training/train.py:145-207) as graph-captured updates of `batch` samples.  Reports the whole round
     (collection + updates) and the collection alone; round 2 is timed (the self-play pool is populated)."""
+    from hockey_amd.td3 import REFERENCE_REPLAY_RATIO as RR
     from hockey_amd.td3 import TD3Config, train, updates_for
 
     cfg = TD3Config(max_steps=steps, start_steps=0)
     table = [(1.0, 0.35, 0.35, 0.30)]  # stage-3's last curriculum row (self-play active from round 2)
     train(n_arenas=n, rounds=2, cfg=TD3Config(max_steps=5, start_steps=0), device=dev, curriculum=table,
-          self_play_interval=n, reset="device", learner_batch=batch)  # warm-up (kernels, graph, allocator)
+          self_play_interval=n, reset="device", learner_batch=batch, replay_ratio=RR)  # warm-up
     agent, st = train(n_arenas=n, rounds=2, cfg=cfg, device=dev, curriculum=table, self_play_interval=n,
-                      reset="device", learner_batch=batch, timing=True)
+                      reset="device", learner_batch=batch, timing=True, replay_ratio=RR)
     collect, update = st["round_time"][1]
-    ups = updates_for(cfg, n, steps, batch)
+    ups = updates_for(cfg, n, steps, batch, RR)
     return {"value": n * steps / (collect + update), "unit": "env-steps/s", "arenas": n, "steps": steps,
             "collect_value": n * steps / collect, "collect_s": collect, "update_s": update,
             "updates": ups, "batch": batch, "samples_per_transition": ups * batch / (n * steps),

@@ -173,6 +173,7 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
   s.final_obs = io->final_obs;
   s.flags = io->flags;
   s.policy2 = io->policy2;
+  s.record = io->record;
   DeviceGuard g(c->device);
   hipError_t e = hk::launch_step(c->s, c->cfg, s, nsteps, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, who);

@@ -46,6 +46,7 @@ struct StepIO {
   float *info, *info2, *actions_out, *debug, *final_obs;
   int flags;
   const uint8_t *policy2;  // per-arena player-2 policy override (hk_step_io.policy2) or nullptr
+  double *record;          // [N,16] f64 step record (hk_step_io.record) or nullptr
 };
 
 hipError_t launch_init(const DevState &s, const KCfg &cfg, hipStream_t st);

@@ -334,6 +334,23 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   }
   if (io.done) io.done[a] = (uint8_t)w.done;
   w.time += 1;
+  if (io.record) {  // the step's float64 values for single-env callers (hk_step_io.record)
+    double i2[4];
+    info_side<1>(w, i2);
+    double *rec = io.record + a * 16;
+    for (int k = 0; k < 4; ++k) {
+      rec[k] = info[k];
+      rec[4 + k] = i2[k];
+    }
+    rec[8] = compute_reward(w) + info[1];
+    rec[9] = -compute_reward(w) + i2[1];
+    rec[10] = w.has1;
+    rec[11] = w.has2;
+    rec[12] = w.time;
+    rec[13] = w.done;
+    rec[14] = w.winner;
+    rec[15] = 0.0;
+  }
   const int done_edge = !was_done && w.done, winner = w.winner;
   if (cfg.auto_reset && w.done) {  // the next episode starts now; obs / obs2 describe its first state
     int one = I(s, I_ONE, a);

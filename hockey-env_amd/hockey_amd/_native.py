@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("HK_LIB") or os.path.join(_HERE, "_lib", "libhockey_hi
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 OBS_DIM, ACT_DIM, INFO_DIM, STATE_DIM, AUX_DIM, PARAM_DIM, DEBUG_DIM, NUM_COUNTERS = 18, 8, 4, 18, 5, 6, 13, 16
+RECORD_DIM = 16
 
 POLICY_EXTERNAL, POLICY_RANDOM, POLICY_BASIC_WEAK, POLICY_BASIC_STRONG = 0, 1, 2, 3
 STEP_SKIP_PHYSICS = 1
@@ -35,7 +36,7 @@ class StepIO(ctypes.Structure):
                 ("obs2", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("reward2", ctypes.c_void_p),
                 ("done", ctypes.c_void_p), ("info", ctypes.c_void_p), ("info2", ctypes.c_void_p),
                 ("actions_out", ctypes.c_void_p), ("debug", ctypes.c_void_p), ("final_obs", ctypes.c_void_p),
-                ("flags", ctypes.c_int32), ("policy2", ctypes.c_void_p)]
+                ("flags", ctypes.c_int32), ("policy2", ctypes.c_void_p), ("record", ctypes.c_void_p)]
 
 
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",

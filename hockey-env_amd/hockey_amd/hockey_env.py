@@ -6,8 +6,10 @@ Same names, constructor arguments, return types and quirks as ``hockey/hockey_en
 one-arena :class:`~hockey_amd.vec_env.VecHockeyEnv`; the step itself always runs on the MI355X.
 
 Every value a facade returns is the kernel's: obs / obs_agent_two from hk_step / hk_observe, and info,
-info_agent_two and both rewards from hk_info in float64, exactly as the reference computes them.  One call
-costs the step launch, the info launch and ONE device-to-host copy of a packed output record.  The fused
+info_agent_two, both rewards and the has_puck / time / done / winner fields in float64 from the step kernel's
+record (hk_step_io.record; hk_info after a reset or set_state), exactly as the reference computes them.  A
+step costs ONE host-to-device copy (action and opponent phase increment packed together), ONE kernel launch
+and ONE device-to-host copy of a packed output record, then one stream synchronisation.  The fused
 ``HockeyEnv_BasicOpponent`` opponent draws its phase from the global ``np.random`` exactly like the
 reference's ``BasicOpponent`` (:785, :796), so seeded reference scripts reproduce.  ``render`` is out of scope.
 """
@@ -24,8 +26,13 @@ from .spaces import Box, Discrete
 __all__ = ["HockeyEnv", "HockeyEnv_BasicOpponent", "BasicOpponent", "PolicyOpponent", "Mode", "register_envs",
            "make"]
 
-# packed per-env output record (one device buffer, one D2H copy): byte offsets
-_OBS, _OBS2, _DONE, _INFO, _INFO2, _REW, _REW2, _AUX, _REC = 0, 72, 144, 152, 184, 216, 224, 232, 256
+# packed per-env output record (one device buffer, one D2H copy): byte offsets.  _F64 holds hk_step_io.record
+# (f64[16]: info, info2, reward, reward2, has1, has2, time, done, winner); hk_info writes its first 10 words
+# after a reset / set_state, and _AUXI the int32 aux of hk_get_state then
+_OBS, _OBS2, _DONE, _F64, _AUXI, _REC = 0, 72, 144, 152, 280, 304
+_INFO, _INFO2, _REW, _REW2 = _F64, _F64 + 32, _F64 + 64, _F64 + 72
+# packed per-step input (one H2D copy): action f32[8], then the opponent's phase increment f64[2]
+_ACT, _INC, _IN = 0, 32, 48
 
 
 def set_state_raw(state, keep_mode=True):
@@ -59,19 +66,21 @@ class HockeyEnv:
         self.seed()
         self._vec = VecHockeyEnv(1, keep_mode=keep_mode, mode=self._mode, device=device, policies=_policies)
         self._rec = torch.zeros(_REC, dtype=torch.uint8, device=self._vec.device)
-        self._act = torch.zeros(N.ACT_DIM, dtype=torch.float32, device=self._vec.device)
-        self._inc = torch.zeros(2, dtype=torch.float64, device=self._vec.device)
+        self._in = torch.zeros(_IN, dtype=torch.uint8, device=self._vec.device)
         # pinned host staging: the per-step transfers are asynchronous copies, one stream sync per step
         self._rec_h = torch.zeros(_REC, dtype=torch.uint8, pin_memory=True)
-        self._act_h = torch.zeros(N.ACT_DIM, dtype=torch.float32, pin_memory=True)
-        self._inc_h = torch.zeros(2, dtype=torch.float64, pin_memory=True)
-        base = self._rec.data_ptr()
+        self._in_h = torch.zeros(_IN, dtype=torch.uint8, pin_memory=True)
+        self._act_h = np.frombuffer(self._in_h.numpy(), np.float32, N.ACT_DIM, _ACT)
+        self._inc_h = np.frombuffer(self._in_h.numpy(), np.float64, 2, _INC)
+        base, ibase = self._rec.data_ptr(), self._in.data_ptr()
         self._io = N.StepIO()
-        self._io.actions = self._act.data_ptr()
+        self._io.actions = ibase + _ACT
         self._io.obs, self._io.obs2, self._io.done = base + _OBS, base + _OBS2, base + _DONE
+        self._io.record = base + _F64
+        self._inc_ptr = ibase + _INC
         self._ptr = {k: ctypes.c_void_p(base + off) for k, off in
                      (("obs", _OBS), ("obs2", _OBS2), ("info", _INFO), ("info2", _INFO2), ("reward", _REW),
-                      ("reward2", _REW2), ("aux", _AUX))}
+                      ("reward2", _REW2), ("aux", _AUXI))}
         self._snap = None
         self.observation_space = Box(-np.inf, np.inf, shape=(18,), dtype=np.float32)
         self.num_actions = 3 if not self.keep_mode else 4
@@ -99,19 +108,23 @@ class HockeyEnv:
 
     # --------------------------------------------------------------- device record
     def _refresh(self, stepped):
-        """Fill the packed record for the current state (info / rewards / aux; obs too unless a step just
-        wrote them) and copy it to the host in one transfer."""
+        """Copy the packed record to the host in one transfer.  After a step the kernel wrote all of it; after a
+        reset / set_state the obs, info / rewards and aux of the current state are filled in first."""
         L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
         p = self._ptr
         if not stepped:
             N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
-        N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
-        N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
+            N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
+            N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
         import torch
 
         self._rec_h.copy_(self._rec, non_blocking=True)
         torch.cuda.current_stream(self._vec.device).synchronize()
         b = self._rec_h.numpy()
+        if stepped:
+            aux = np.frombuffer(b, np.float64, 5, _F64 + 80).astype(np.int32)
+        else:
+            aux = np.frombuffer(b, np.int32, 5, _AUXI).copy()
         self._snap = {
             "obs": np.frombuffer(b, np.float32, 18, _OBS).astype(np.float64),
             "obs2": np.frombuffer(b, np.float32, 18, _OBS2).astype(np.float64),
@@ -119,7 +132,7 @@ class HockeyEnv:
             "info2": np.frombuffer(b, np.float64, 4, _INFO2).copy(),
             "reward": float(np.frombuffer(b, np.float64, 1, _REW)[0]),
             "reward2": float(np.frombuffer(b, np.float64, 1, _REW2)[0]),
-            "aux": np.frombuffer(b, np.int32, 5, _AUX).copy()}
+            "aux": aux}
         return self._snap
 
     # --------------------------------------------------------------- reset / step
@@ -143,15 +156,14 @@ class HockeyEnv:
         return self._obs_out(s["obs"]), self._get_info()
 
     def _launch_step(self, a8, opp_inc=None):
-        # the previous step ended with a stream sync, so the pinned staging buffers are free to reuse
-        self._act_h.numpy()[:] = a8
-        self._act.copy_(self._act_h, non_blocking=True)
+        # the previous step ended with a stream sync, so the pinned staging buffer is free to reuse
+        self._act_h[:] = a8
         io = self._io
         io.opp_inc = None
         if opp_inc is not None:
-            self._inc_h.numpy()[:] = opp_inc
-            self._inc.copy_(self._inc_h, non_blocking=True)
-            io.opp_inc = self._inc.data_ptr()
+            self._inc_h[:] = opp_inc
+            io.opp_inc = self._inc_ptr
+        self._in.copy_(self._in_h, non_blocking=True)
         N.check(self._vec.L.hk_step(self._vec._ctx, ctypes.byref(io), self._vec._stream()), "hk_step")
         s = self._refresh(stepped=True)
         return self._obs_out(s["obs"]), s["reward"], s["done"], False, self._info_dict(s["info"])

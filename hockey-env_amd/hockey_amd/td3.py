@@ -428,12 +428,12 @@ class Learner:
 
 def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_per_round=None, mode=Mode.NORMAL,
           curriculum=None, use_self_play=None, self_play_interval=None, pool_size=None, reset="seeded", log=None,
-          replay_capacity=None, graphs=True, eval_fn=None, learner_batch=None, timing=False):
+          replay_capacity=None, graphs=True, eval_fn=None, learner_batch=None, timing=False, replay_ratio=None):
     """Batched TD3 training (rl/training/train.py TD3Trainer.train).  Each round runs ``max_steps`` steps of
     ``n_arenas`` parallel episodes (no break on done), stores every transition, then performs the learner
-    updates of those episodes at the reference's replay ratio: ``cfg.replay_ratio * n_arenas * max_steps /
-    batch_size`` updates (= ``train_iters`` per episode at the reference's batch), unless ``updates_per_round``
-    overrides it.  Player 2 follows the curriculum's opponent mix (``hockey_amd.opponents.OpponentMix``),
+    updates of those episodes at the replay ratio: ``ratio * n_arenas * max_steps / B`` updates of batch B =
+    ``learner_batch`` (default ``cfg.batch_size``), ratio = ``replay_ratio`` (default ``cfg.replay_ratio``:
+    ``train_iters`` per episode at the config's batch), unless ``updates_per_round`` overrides it.  Player 2 follows the curriculum's opponent mix (``hockey_amd.opponents.OpponentMix``),
     re-drawn per arena and step.
 
     Replay capacity: ``cfg.buffer_size``, raised to one full round of every arena (``n_arenas * max_steps``)
@@ -464,7 +464,7 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     batch = int(learner_batch or cfg.batch_size)
     learner = Learner(agent, ring, batch, graphs=graphs)
     updates = updates_per_round if updates_per_round is not None else \
-        updates_for(cfg, n_arenas, cfg.max_steps, batch)
+        updates_for(cfg, n_arenas, cfg.max_steps, batch, replay_ratio)
     act8 = torch.zeros((n_arenas, 8), device=device)
     stats = {"env_steps": 0, "updates": 0, "updates_per_round": updates, "batch": batch,
              "replay_ratio": updates * batch / (n_arenas * cfg.max_steps),
@@ -525,10 +525,14 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     return agent, stats
 
 
-def updates_for(cfg, n_arenas, steps, batch=None):
-    """Learner updates that follow ``steps`` collection steps of ``n_arenas`` at the config's replay ratio
-    (``cfg.replay_ratio`` samples per stored transition), drawn as batches of ``batch`` (default
-    ``cfg.batch_size``): the reference's 32 updates per 500-step episode at batch 256, proportionally fewer
-    updates of a larger batch."""
+REFERENCE_REPLAY_RATIO = 32 * 256 / 500  # train_iters x batch_size per max_steps-step episode (config.py defaults)
+
+
+def updates_for(cfg, n_arenas, steps, batch=None, ratio=None):
+    """Learner updates that follow ``steps`` collection steps of ``n_arenas`` at ``ratio`` samples per stored
+    transition (default ``cfg.replay_ratio``; rounds shorter than an episode pass the reference's
+    ``REFERENCE_REPLAY_RATIO``), drawn as batches of ``batch`` (default ``cfg.batch_size``): the reference's 32
+    updates per 500-step episode at batch 256, proportionally fewer updates of a larger batch."""
     b = int(batch or cfg.batch_size)
-    return max(1, int(math.floor(cfg.replay_ratio * n_arenas * steps / b + 0.5)))
+    r = cfg.replay_ratio if ratio is None else float(ratio)
+    return max(1, int(math.floor(r * n_arenas * steps / b + 0.5)))

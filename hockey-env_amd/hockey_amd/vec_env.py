@@ -36,7 +36,7 @@ def _policy_id(p):
 
 
 class StepResult:
-    __slots__ = ("obs", "reward", "done", "info", "obs2", "reward2", "info2", "actions", "final_obs")
+    __slots__ = ("obs", "reward", "done", "info", "obs2", "reward2", "info2", "actions", "final_obs", "record")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -87,6 +87,7 @@ class VecHockeyEnv:
         self.info2_buf = torch.zeros((n, N.INFO_DIM), dtype=torch.float32, device=d)
         self.actions_buf = torch.zeros((n, N.ACT_DIM), dtype=torch.float32, device=d)
         self.final_obs_buf = torch.zeros((n, N.OBS_DIM), dtype=torch.float32, device=d)
+        self.record_buf = torch.zeros((n, N.RECORD_DIM), dtype=torch.float64, device=d)
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -146,7 +147,7 @@ class VecHockeyEnv:
 
     # ------------------------------------------------------------------ step
     def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=None, skip_physics=False,
-             record_actions=False, final_obs=False, policy2=None):
+             record_actions=False, final_obs=False, policy2=None, record=False):
         """HockeyEnv.step for every arena.  actions: [N,8] float (clipped in-kernel), may be None when no
         player is external.  Returns a StepResult of device tensors (views of persistent buffers).
 
@@ -156,7 +157,10 @@ class VecHockeyEnv:
 
         policy2 ([N] uint8 / policy ids, optional): player 2's policy of each arena for this step, overriding
         the context's (rl/training/opponent_manager.py draws the opponent per step); 'external' arenas read
-        actions[:, 4:8]."""
+        actions[:, 4:8].
+
+        record: also return the [N,16] float64 step record (include/hockey.h hk_step_io.record: info, info2,
+        reward, reward2 in float64 and has_puck1/2, time, done, winner after the step)."""
         a = None
         if actions is not None:
             a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
@@ -183,6 +187,8 @@ class VecHockeyEnv:
             io.debug = debug.data_ptr()
         if final_obs:
             io.final_obs = self.final_obs_buf.data_ptr()
+        if record:
+            io.record = self.record_buf.data_ptr()
         io.flags = N.STEP_SKIP_PHYSICS if skip_physics else 0
         p2 = None
         if policy2 is not None:
@@ -196,7 +202,8 @@ class VecHockeyEnv:
                           reward2=self.reward2_buf if with_agent_two else None,
                           info2=self.info2_buf if with_agent_two else None,
                           actions=self.actions_buf if record_actions else None,
-                          final_obs=self.final_obs_buf if final_obs else None)
+                          final_obs=self.final_obs_buf if final_obs else None,
+                          record=self.record_buf if record else None)
 
     def step_raw(self, io):
         """Launch one step with a prepared StepIO (no Python-side allocation; for benchmarks)."""

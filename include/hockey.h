@@ -34,6 +34,7 @@ extern "C" {
 #define HK_PARAM_DIM 6  /* reset placement: p2x, p2y, puckx, pucky, puck_fx, puck_fy */
 #define HK_DEBUG_DIM 13 /* pre-solve F1xy, F2xy, Fpuck xy, tau1, tau2, ldamp1,2,puck, adamp1,2 */
 #define HK_NUM_COUNTERS 16
+#define HK_RECORD_DIM 16 /* hk_step_io.record: f64 per arena */
 
 enum {
   HK_OK = 0,
@@ -112,6 +113,13 @@ typedef struct hk_step_io {
                              above 3 is counted in HK_CNT_BAD_POLICY and that player acts with zeros.
                              Under an override the strong bot keeps phase row 1 and the weak bot its own row 2
                              (the reference's OpponentManager holds one BasicOpponent of each kind) */
+  double *record;         /* [N,16] f64 per-step record (or NULL), the float64 values the reference's step
+                             returns, written by the step kernel so a single-env caller needs one launch and
+                             one copy: [0:4] info {winner, closeness, touch, direction} (_get_info), [4:8]
+                             info2 (get_info_agent_two), [8] reward (get_reward(info)), [9] reward2
+                             (get_reward_agent_two(info2)), [10] has_puck1, [11] has_puck2, [12] time, [13]
+                             done, [14] winner -- after the step, before any auto-reset -- [15] 0.
+                             hockey_env.py:542-591, 518-540, 685-693 */
 } hk_step_io;
 
 const char *hk_last_error(void);

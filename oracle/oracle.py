@@ -66,6 +66,7 @@ def lib():
         L.hkov_counters.argtypes = [vp, vp]
         L.hkov_time_steps.restype = ctypes.c_double
         L.hkov_time_steps.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.hko_set_variant.argtypes = [ctypes.c_int]
         L.hko_run_c1.restype = ctypes.c_int
         L.hko_run_c1.argtypes = [ctypes.c_int, _f32p, _f64p, ctypes.c_double, _f32p, ctypes.c_int, vp, vp,
                                  ctypes.POINTER(ctypes.c_double)]
@@ -136,6 +137,15 @@ class OracleWorld:
         o = np.zeros(4, np.int32)
         self._L.hko_stats(self._w, o)
         return o
+
+
+VAR_REVERSE, VAR_NO_BLOCK, VAR_NO_SLEEP, VAR_ITERS_8_3 = 1, 2, 4, 8
+
+
+def set_variant(flags):
+    """Process-wide sensitivity-study variant of the Box2D restatement (hk_oracle.c hko_set_variant); 0 restores
+    the restatement the kernel is pinned to."""
+    lib().hko_set_variant(int(flags))
 
 
 def basic_opponent(weak, keep_mode, phase, inc, obs18):

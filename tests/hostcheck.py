@@ -56,7 +56,7 @@ def _p(a):
 class StepIO(ctypes.Structure):
     _fields_ = [(k, ctypes.c_void_p) for k in ("actions", "opp_inc", "obs", "obs2", "reward", "reward2", "done",
                                                "info", "info2", "actions_out", "debug", "final_obs")] + [
-                    ("flags", ctypes.c_int32), ("policy2", ctypes.c_void_p)]
+                    ("flags", ctypes.c_int32), ("policy2", ctypes.c_void_p), ("record", ctypes.c_void_p)]
 
 
 POLICY = {"external": 0, "random": 1, "weak": 2, "strong": 3}
@@ -93,7 +93,7 @@ class HostVec:
         self.L.hkh_reset(self.h, _p(m), _p(p), _p(mt), None)
 
     def step(self, actions=None, with_agent_two=False, opp_inc=None, debug=False, skip_physics=False,
-             record_actions=False, final_obs=False, policy2=None):
+             record_actions=False, final_obs=False, policy2=None, record=False):
         n = self.n
         out = SimpleNamespace(obs=np.zeros((n, 18), np.float32), reward=np.zeros(n, np.float32),
                               done=np.zeros(n, np.uint8), info=np.zeros((n, 4), np.float32))
@@ -115,6 +115,9 @@ class HostVec:
         if final_obs:
             out.final_obs = np.zeros((n, 18), np.float32)
             io.final_obs = _p(out.final_obs)
+        if record:
+            out.record = np.zeros((n, 16), np.float64)
+            io.record = _p(out.record)
         io.flags = 1 if skip_physics else 0
         p2 = None if policy2 is None else np.ascontiguousarray(policy2, np.uint8)
         io.policy2 = _p(p2)

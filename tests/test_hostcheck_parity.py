@@ -175,3 +175,25 @@ def test_live_velocity_semantics_with_physics_vs_oracle_vec(oracle):
     assert "field" not in out, out
     out = _vec_lockstep(oracle, 48, 300, 1, ("strong", "strong"), seed=48, vel_ref=True)
     assert "field" not in out, out
+
+
+def test_step_record_matches_outputs_and_state(oracle):
+    """hk_step_io.record (the single-env facade's one-copy step result): float64 info / info2 / rewards whose
+    float32 roundings are the step's float outputs (oracle-checked), and has_puck / time / done / winner equal
+    to the state after the step -- over a strong-vs-strong run with goals and holds."""
+    n = 64
+    env = HostVec(n, policies=("strong", "strong"), auto_reset=False, seed=9)
+    ov = oracle.OracleVec(n, policies=("strong", "strong"), auto_reset=False, seed=9)
+    held = 0
+    for t in range(300):
+        got = env.step(None, with_agent_two=True, record=True)
+        want = ov.step(with_agent_two=True)
+        rec = got.record
+        assert first_mismatch(t, {"info": rec[:, 0:4].astype(np.float32), "info2": rec[:, 4:8].astype(np.float32),
+                                  "reward": rec[:, 8].astype(np.float32), "reward2": rec[:, 9].astype(np.float32)},
+                              want, fields=("info", "info2", "reward", "reward2")) is None
+        _, aux = env.get_state()
+        assert np.array_equal(rec[:, 10:15].astype(np.int32), aux), t
+        assert np.array_equal(rec[:, 13].astype(np.uint8), got.done) and np.all(rec[:, 15] == 0)
+        held += int((aux[:, 0] > 0).sum())
+    assert aux[:, 3].sum() > 0 and held > 0  # goals and holds happened

@@ -11,7 +11,8 @@ import os
 
 from hockey_amd.evaluate import load_actor
 from hockey_amd.noise import GaussianNoise, OrnsteinUhlenbeckNoise, PinkNoise, UniformNoise, make_noise
-from hockey_amd.td3 import TD3, Learner, PrioritizedRing, ReplayRing, TD3Config, smooth_l1, updates_for
+from hockey_amd.td3 import (REFERENCE_REPLAY_RATIO, TD3, Learner, PrioritizedRing, ReplayRing, TD3Config, smooth_l1,
+                            updates_for)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -195,6 +196,8 @@ def test_stage1_config_and_replay_ratio():
     assert updates_for(cfg, 1, 500) == 32  # train_iters per 500-step episode at the reference's batch
     assert updates_for(cfg, 20, 500) == 640
     assert updates_for(cfg, 65536, 50, batch=16384) == round(16.384 * 65536 * 50 / 16384)
+    short = TD3Config(max_steps=50)  # a 50-step round at the reference's ratio, not 32 updates per 50 steps
+    assert updates_for(short, 65536, 50, batch=16384, ratio=REFERENCE_REPLAY_RATIO) == 3277
 
 
 def test_learner_eager_updates_on_cpu():
@@ -278,10 +281,11 @@ def test_c5_training_loop_65536_arenas_with_opponent_mix():
     n, rounds, steps = 65536, 3, 40
     cfg = TD3Config(max_steps=steps, start_steps=0, batch_size=256)
     agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, seed=5, learner_batch=16384,
-                      curriculum=[(1.0, 0.35, 0.35, 0.30)], self_play_interval=n, pool_size=2)
+                      replay_ratio=REFERENCE_REPLAY_RATIO, curriculum=[(1.0, 0.35, 0.35, 0.30)],
+                      self_play_interval=n, pool_size=2)
     assert st["env_steps"] == rounds * steps * n
     assert st["replay_capacity"] == n * steps and st["replay_size"] == n * steps
-    ups = updates_for(cfg, n, steps, batch=16384)
+    ups = updates_for(cfg, n, steps, batch=16384, ratio=REFERENCE_REPLAY_RATIO)
     assert ups == round(16.384 * n * steps / 16384) and st["updates"] == rounds * ups
     assert abs(st["replay_ratio"] - 16.384) < 0.01
     assert all(np.isfinite(st["critic_loss"])) and all(np.isfinite(st["actor_loss"]))
