@@ -57,8 +57,12 @@ constexpr uint32_t pair_mask_of_scene(bool toi) {
 static_assert(pair_mask_of_scene(true) == kToiPairs && pair_mask_of_scene(false) == kSensorMask,
               "pair masks follow the compiled scene's pair table");
 
-// LDS per lane: [0,27) TOI alpha per pair, [27,35) static sweep alpha0, [35,62) TOI sub-step count
+// LDS per lane: [0,27) TOI alpha per pair, [27,35) static sweep alpha0, [35,62) TOI sub-step count; then,
+// per wave, the work list of the cooperative b2TimeOfImpact drain (toi_drain_wave): kToiQ items of
+// kToiItemWords words
 constexpr int kLdsToi = 0, kLdsSal0 = 27, kLdsCnt = 35, kLdsPerLane = 62;
+constexpr int kToiQ = 128, kToiItemWords = 9;
+constexpr int kLdsWords = kLdsPerLane * 64 + kToiQ * kToiItemWords;
 
 struct Dyn {
   float px[3], py[3], qs[3], qc[3];      // transform (origin, rotation)
@@ -761,18 +765,21 @@ HK_DEV void toi_island_solve(Arena &w, SL &S, int minc, uint32_t extra, int nc, 
   sync_xf(w, db);
 }
 
-// b2TimeOfImpact of static-vs-dynamic pair p (per-lane p) -> alpha in the step's [alpha0, 1] frame
-HK_DEV float toi_pair(Arena &w, int p) {
-  const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
-  const float alpha0 = pick(w.d.al0, bB, 0.0f);  // == max(alpha0 A, alpha0 B) after alignment
+// b2TimeOfImpact of static-vs-dynamic pair p from the two sweeps -> alpha in the step's [alpha0, 1] frame
+// (sB.alpha0 == max(alpha0 A, alpha0 B) after alignment)
+HK_DEV float toi_pair_sweeps(int p, const Sweep &sA, const Sweep &sB) {
   const Proxy<kStaticVerts, true> pA = make_proxy<kStaticVerts, true>(SLDS.fx[SLDS.pairA[p]]);
   const Proxy<kMaxPolyVerts> pB = make_proxy<kMaxPolyVerts>(SLDS.fx[SLDS.pairB[p]]);
   float beta;
-  const int st = time_of_impact(pA, pB, body_sweep(w, bA), body_sweep(w, bB), 1.0f, beta);
+  const int st = time_of_impact(pA, pB, sA, sB, 1.0f, beta);
+  return st == TOI_TOUCHING ? fmin2(sB.alpha0 + (1.0f - sB.alpha0) * beta, 1.0f) : 1.0f;
+}
+// per-lane pair p of this lane's arena
+HK_DEV float toi_pair(Arena &w, int p) {
 #ifdef HK_PHASE_TIMERS
   w.dg_toi_calls++;
 #endif
-  return st == TOI_TOUCHING ? fmin2(alpha0 + (1.0f - alpha0) * beta, 1.0f) : 1.0f;
+  return toi_pair_sweeps(p, body_sweep(w, SLDS.pbodyA[p]), body_sweep(w, SLDS.pbodyB[p]));
 }
 // runs the lane's queued b2TimeOfImpact calls in pair order; `below` tracks the pairs whose cached alpha is
 // below 1 (the only ones the minimum selection can pick: it starts at 1 and compares strictly)
@@ -784,6 +791,83 @@ HK_DEV void toi_drain(Arena &w, uint32_t &pending, uint32_t &below) {
     LDS(w, kLdsToi + p) = alpha;
     below = alpha < 1.0f ? (below | (1u << p)) : (below & ~(1u << p));
   }
+}
+
+// Cooperative drain (device build; every lane of the wave that runs the step calls it, with or without queued
+// pairs).  A per-lane queue holds the wave for as many rounds as its longest queue; here the wave's queued
+// (lane, pair) calls are listed in LDS -- pair id, owner lane and the two sweeps' inputs, copied at this point
+// -- and dealt out to all lanes, so a lane with k queued pairs no longer costs k rounds.  A worker writes alpha
+// into the owner's TOI cache slot; the owner then updates `below`.  The calls are independent (each reads only
+// its own pair's sweeps, which nothing changes until the drain is over), and a worker runs the same arithmetic
+// on the same inputs as the owner would: bit-identical alphas.  The host build (one lane at a time) drains per
+// lane.
+HK_DEV void toi_drain_wave(Arena &w, uint32_t &pending, uint32_t &below) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float *q = w.lds + kLdsPerLane * 64;
+  const uint64_t lt = (1ull << w.lane) - 1ull;  // lanes below this one
+  while (wave_any(pending != 0u)) {
+    // exclusive prefix sum of the lanes' queue lengths (<= 27: five bit-planes of ballots)
+    const int cnt = __popc(pending);
+    int off = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const uint64_t m = __ballot((cnt >> b) & 1);
+      off += __popcll(m & lt) << b;
+      total += __popcll(m) << b;
+    }
+    uint32_t listed = 0u;
+    for (uint32_t m = pending; m && off < kToiQ; m &= m - 1u, ++off) {
+      const int p = __ffs(m) - 1;
+      const Sweep sB = body_sweep(w, SLDS.pbodyB[p]);
+      float *it = q + off * kToiItemWords;
+      it[0] = __int_as_float(p | (w.lane << 8));
+      it[1] = sB.c0.x;
+      it[2] = sB.c0.y;
+      it[3] = sB.c.x;
+      it[4] = sB.c.y;
+      it[5] = sB.a0;
+      it[6] = sB.a;
+      it[7] = sB.alpha0;
+      it[8] = LDS(w, kLdsSal0 + SLDS.pbodyA[p] - 3);  // the static body's alpha0
+      listed |= m & (0u - m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int n = total < kToiQ ? total : kToiQ;
+    for (int k = w.lane; k < n; k += 64) {
+      const float *it = q + k * kToiItemWords;
+      const int tag = __float_as_int(it[0]), p = tag & 255, owner = tag >> 8;
+      const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
+      Sweep sA, sB;
+      sA.lc = V(0.0f, 0.0f);
+      sA.c0 = sA.c = V(SLDS.spx[bA], SLDS.spy[bA]);
+      sA.a0 = sA.a = 0.0f;
+      sA.alpha0 = it[8];
+      sB.lc = local_center(bB);
+      sB.c0 = V(it[1], it[2]);
+      sB.c = V(it[3], it[4]);
+      sB.a0 = it[5];
+      sB.a = it[6];
+      sB.alpha0 = it[7];
+      w.lds[(kLdsToi + p) * 64 + owner] = toi_pair_sweeps(p, sA, sB);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef HK_PHASE_TIMERS
+    w.dg_toi_calls += __popc(listed);
+#endif
+    pending &= ~listed;
+    for (uint32_t m = listed; m; m &= m - 1u) {
+      const int p = __ffs(m) - 1;
+      const float alpha = LDS(w, kLdsToi + p);
+      below = alpha < 1.0f ? (below | (1u << p)) : (below & ~(1u << p));
+    }
+  }
+#else
+  toi_drain(w, pending, below);
+#endif
 }
 
 HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
@@ -798,79 +882,85 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
   uint32_t exhausted = 0u;  // pairs past b2_maxSubSteps TOI events this step (toi_count > 8, kept in LDS)
   uint32_t redo = 0u;       // pairs a later scan pass must visit: the last event's body's contacts
   bool first = true;
-  for (;;) {
+  // The lanes stay together in this loop until every lane is done (`act`), so that the b2TimeOfImpact calls
+  // of step (2) can be dealt out over the whole wave (toi_drain_wave).  A lane that is done only contributes
+  // worker capacity.
+  bool act = true;
+  while (wave_any(act)) {
     HK_TIC(T, 5);  // diagnostics: events / min selection -> "toi-events"
-    // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
-    //     far rejection.  Pairs that need a real b2TimeOfImpact are queued per lane.  During a step the
-    //     alignment only ever advances a STATIC body's alpha0 (TOI events come in non-decreasing alpha, and
-    //     only the moved body's pairs are re-evaluated, so a0(static) <= a0(dynamic) for them); the queued
-    //     TOIs therefore see exactly the sweeps the sequential scan would.  Should a dynamic body ever be
-    //     advanced here, its lane first drains its queue so the sequential order is kept regardless.
     uint32_t elig = 0u, pending = 0u;
-    CoreBoxes cb;  // the players' poses are fixed during the pass (only sweep starts move)
-    core_boxes(w, cb);
-    uint32_t todo;
-    if (first) {
-      uint32_t settled = 0u;
-      // The first pass has no order-dependent side effect (every alpha0 is still 0, so the alignment is a
-      // no-op): the TOI pairs of a body inside its interior rectangle are settled in bulk as eligible with
-      // alpha 1, exactly what the per-pair pass below would record for them.
+    if (act) {
+      // (1) In pair order: eligibility, sweep alignment (the only order-dependent side effect) and the cheap
+      //     far rejection.  Pairs that need a real b2TimeOfImpact are queued.  During a step the alignment
+      //     only ever advances a STATIC body's alpha0 (TOI events come in non-decreasing alpha, and only the
+      //     moved body's pairs are re-evaluated, so a0(static) <= a0(dynamic) for them); the queued TOIs
+      //     therefore see exactly the sweeps the sequential scan would.  Should a dynamic body ever be
+      //     advanced here, its lane first drains its queue so the sequential order is kept regardless.
+      CoreBoxes cb;  // the players' poses are fixed during the pass (only sweep starts move)
+      core_boxes(w, cb);
+      uint32_t todo;
+      if (first) {
+        uint32_t settled = 0u;
+        // The first pass has no order-dependent side effect (every alpha0 is still 0, so the alignment is a
+        // no-op): the TOI pairs of a body inside its interior rectangle are settled in bulk as eligible with
+        // alpha 1, exactly what the per-pair pass below would record for them.
 #pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const float lx = fminf(w.d.c0x[b], w.d.cx[b]), ly = fminf(w.d.c0y[b], w.d.cy[b]);
-        const float hx = fmaxf(w.d.c0x[b], w.d.cx[b]), hy = fmaxf(w.d.c0y[b], w.d.cy[b]);
-        bool in;
-        if (b == B_PK) {
-          in = inside(kInteriorPuck, lx, ly, hx, hy);  // a circle's core is its centre
-        } else {
-          const float(&e)[4] = cb.e[b];
-          const float rot = SC.rcore[b] * fabsf(w.d.a[b] - w.d.a0[b]);
-          in = inside(kInteriorPlayer, lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot);
+        for (int b = 0; b < 3; ++b) {
+          const float lx = fminf(w.d.c0x[b], w.d.cx[b]), ly = fminf(w.d.c0y[b], w.d.cy[b]);
+          const float hx = fmaxf(w.d.c0x[b], w.d.cx[b]), hy = fmaxf(w.d.c0y[b], w.d.cy[b]);
+          bool in;
+          if (b == B_PK) {
+            in = inside(kInteriorPuck, lx, ly, hx, hy);  // a circle's core is its centre
+          } else {
+            const float(&e)[4] = cb.e[b];
+            const float rot = SC.rcore[b] * fabsf(w.d.a[b] - w.d.a0[b]);
+            in = inside(kInteriorPlayer, lx + e[0] - rot, ly + e[1] - rot, hx + e[2] + rot, hy + e[3] + rot);
+          }
+          if (in && w.d.awake[b]) settled |= kEdgeMask[b];
         }
-        if (in && w.d.awake[b]) settled |= kEdgeMask[b];
-      }
-      settled &= kToiPairs & w.enabled;
-      elig |= settled;
-      w.toiflag |= settled;
-      below &= ~settled;
-      todo = kToiPairs & w.enabled & ~settled;
-    } else {
-      // Later passes: an event re-enables TOI only on the moved dynamic body's contacts (their flags were
-      // cleared).  Every other pair keeps its eligibility and cached alpha (cached pairs are eligible;
-      // the rest were skipped for reasons no event changes), so only `redo` is visited.
-      elig = w.toiflag & w.enabled & ~exhausted;
-      todo = redo & kToiPairs & w.enabled & ~exhausted & ~w.toiflag;
-    }
-    // in pair order, per lane: eligibility, sweep alignment and the far test of the pairs still open
-    while (todo) {
-      const int p = __ffs(todo) - 1;
-      todo &= todo - 1u;
-      const uint32_t bit = 1u << p;
-      const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
-      if (!pick(w.d.awake, bB, 0)) continue;
-      elig |= bit;
-      w.toiflag |= bit;
-      const float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
-      if (a0A < a0B) {
-        LDS(w, kLdsSal0 + bA - 3) = a0B;  // static b2Sweep::Advance: only alpha0 moves
-      } else if (a0B < a0A) {
-        toi_drain(w, pending, below);  // keep the sequential order for this lane (see above)
-        Sweep sw = body_sweep(w, bB);
-        sweep_advance(sw, a0A);
-        body_set_sweep(w, bB, sw);
-      }
-      if (pair_far_toi(w, p, cb, SLDS)) {
-        below &= ~bit;
+        settled &= kToiPairs & w.enabled;
+        elig |= settled;
+        w.toiflag |= settled;
+        below &= ~settled;
+        todo = kToiPairs & w.enabled & ~settled;
       } else {
-        pending |= bit;
+        // Later passes: an event re-enables TOI only on the moved dynamic body's contacts (their flags were
+        // cleared).  Every other pair keeps its eligibility and cached alpha (cached pairs are eligible;
+        // the rest were skipped for reasons no event changes), so only `redo` is visited.
+        elig = w.toiflag & w.enabled & ~exhausted;
+        todo = redo & kToiPairs & w.enabled & ~exhausted & ~w.toiflag;
       }
+      // in pair order, per lane: eligibility, sweep alignment and the far test of the pairs still open
+      while (todo) {
+        const int p = __ffs(todo) - 1;
+        todo &= todo - 1u;
+        const uint32_t bit = 1u << p;
+        const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
+        if (!pick(w.d.awake, bB, 0)) continue;
+        elig |= bit;
+        w.toiflag |= bit;
+        const float a0A = LDS(w, kLdsSal0 + bA - 3), a0B = pick(w.d.al0, bB, 0.0f);
+        if (a0A < a0B) {
+          LDS(w, kLdsSal0 + bA - 3) = a0B;  // static b2Sweep::Advance: only alpha0 moves
+        } else if (a0B < a0A) {
+          toi_drain(w, pending, below);  // keep the sequential order for this lane (see above)
+          Sweep sw = body_sweep(w, bB);
+          sweep_advance(sw, a0A);
+          body_set_sweep(w, bB, sw);
+        }
+        if (pair_far_toi(w, p, cb, SLDS)) {
+          below &= ~bit;
+        } else {
+          pending |= bit;
+        }
+      }
+      first = false;
     }
-    first = false;
     HK_TIC(T, 6);  // diagnostics: scan pass -> "toi-scan"
-    // (2) per-lane queue: every lane runs b2TimeOfImpact on its own next pair (lanes stay converged on
-    //     the same code instead of serialising over the union of the wave's pairs)
-    toi_drain(w, pending, below);
+    // (2) the queued b2TimeOfImpact calls of the whole wave, dealt out over all its lanes
+    toi_drain_wave(w, pending, below);
     HK_TIC(T, 7);  // diagnostics: b2TimeOfImpact -> "toi-solve" slot
+    if (!act) continue;
     // (3) Box2D's minimum: first pair (in order) with the smallest alpha.  Pairs at alpha 1 never win the
     //     strict comparison, so only the lane's eligible pairs below 1 are visited (usually none or one).
     int minc = -1;
@@ -880,7 +970,10 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
       const float alpha = LDS(w, kLdsToi + p);
       if (alpha < minAlpha) { minc = p; minAlpha = alpha; }
     }
-    if (minc < 0 || 1.0f - 10.0f * kFltEps < minAlpha) break;
+    if (minc < 0 || 1.0f - 10.0f * kFltEps < minAlpha) {
+      act = false;
+      continue;
+    }
     // ---- one TOI event (per-lane pair) ----
     const int bA = SLDS.pbodyA[minc], bB = SLDS.pbodyB[minc];  // static A, dynamic B
     const uint32_t mbit = 1u << minc;

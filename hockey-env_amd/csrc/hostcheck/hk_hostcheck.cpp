@@ -66,7 +66,7 @@ void *hkh_create(int64_t n, const int *cfg6, uint64_t seed, int64_t arena_offset
   c->man.assign((size_t)NSOLID * NMF * n, 0.0f);
   c->phase.assign((size_t)3 * n, 0.0);
   c->counters.assign(16, 0ull);
-  c->lds.assign((size_t)kLdsPerLane * 64, 0.0f);
+  c->lds.assign((size_t)kLdsWords, 0.0f);
   c->s.f = c->f.data();
   c->s.i = c->i.data();
   c->s.man = c->man.data();

@@ -54,13 +54,15 @@ def load_actor(path_or_state, device="cuda:0"):
     return actor.to(device).eval()
 
 
-def reset_params(episodes, seed, mode=Mode.NORMAL):
-    """Placement of episode i as ``env.reset(seed=seed + i)`` on a reused reference env."""
+def reset_params(episodes, seed, mode=Mode.NORMAL, first_reset=0):
+    """Placement of episode i as ``env.reset(seed=seed + i)`` on a reused reference env whose
+    ``first_reset + i``-th reset (0-based, after the constructor's) it is: ``one_starts`` toggles on every
+    reset from the constructor's True, so it is False on the even ones."""
     params = np.zeros((episodes, 6), np.float32)
     one = np.zeros(episodes, bool)
     for i in range(episodes):
         rng, _ = np_random(seed + i)
-        one[i] = (i % 2) == 1
+        one[i] = ((first_reset + i) % 2) == 1
         params[i], max_t = placement(mode, bool(one[i]), rng)
     return params, max_t, one
 

@@ -244,13 +244,13 @@ class PrioritizedRing(ReplayRing):
 
 
 class TD3:
-    def __init__(self, cfg=None, device="cuda:0", seed=0, max_total_steps=None, n_envs=1, noise_seed=None):
+    def __init__(self, cfg=None, device="cuda:0", seed=0, max_total_steps=None, n_envs=1, noise_seed=None, h=256):
         self.cfg = cfg or TD3Config()
         self.device = torch.device(device)
         self.seed = seed
         torch.manual_seed(seed)
-        self.actor, self.critic = Actor().to(self.device), TwinQ().to(self.device)
-        self.target_actor, self.target_critic = Actor().to(self.device), TwinQ().to(self.device)
+        self.actor, self.critic = Actor(h=h).to(self.device), TwinQ(h=h).to(self.device)
+        self.target_actor, self.target_critic = Actor(h=h).to(self.device), TwinQ(h=h).to(self.device)
         self.target_actor.load_state_dict(self.actor.state_dict())
         self.target_critic.load_state_dict(self.critic.state_dict())
         for net in (self.target_actor, self.target_critic):
@@ -331,16 +331,17 @@ class TD3:
             raise ValueError("Unknown anneal mode")
         return max(scale, c.noise_min_scale)
 
-    def act(self, obs, noise=True):
+    def act(self, obs, noise=True, count=None):
         """get_action for a batch of arenas (one call per arena, in arena order): the agent's step count
-        advances by N; arena i's action is uniform random while its step index is below start_steps, else
-        actor + exploration noise (noise=False: eval_mode, no count, no noise)."""
+        advances by N (or ``count``: the arenas whose episode is still running); arena i's action is uniform
+        random while its step index is below start_steps, else actor + exploration noise (noise=False:
+        eval_mode, no count, no noise)."""
         n = obs.shape[0]
         if not noise:
             with torch.no_grad():
                 return self.actor(obs)
         first = self.total_steps + 1  # arena 0's total_steps after its increment
-        self.total_steps += n
+        self.total_steps += n if count is None else int(count)
         c = self.cfg
         if self.total_steps < c.start_steps:  # every arena of the batch is in the random phase
             return torch.rand((n, 4), device=obs.device) * 2 - 1
@@ -428,7 +429,8 @@ class Learner:
 
 def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_per_round=None, mode=Mode.NORMAL,
           curriculum=None, use_self_play=None, self_play_interval=None, pool_size=None, reset="seeded", log=None,
-          replay_capacity=None, graphs=True, eval_fn=None, learner_batch=None, timing=False, replay_ratio=None):
+          replay_capacity=None, graphs=True, eval_fn=None, learner_batch=None, timing=False, replay_ratio=None,
+          env=None, on_step=None, episode_end="max_steps"):
     """Batched TD3 training (rl/training/train.py TD3Trainer.train).  Each round runs ``max_steps`` steps of
     ``n_arenas`` parallel episodes (no break on done), stores every transition, then performs the learner
     updates of those episodes at the replay ratio: ``ratio * n_arenas * max_steps / B`` updates of batch B =
@@ -443,7 +445,17 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     arenas); "device" uses the kernel's Philox placement (same distribution, no host work).
     eval_fn(agent, episodes_done) is called every ``cfg.eval_interval`` episodes.  timing: synchronise around each
     round's collection and updates and record their wall seconds in ``stats["round_time"]``.  Returns
-    (agent, stats)."""
+    (agent, stats).  env: a VecHockeyEnv-shaped batch of n_arenas arenas to train on (default: a new
+    VecHockeyEnv on ``device``; the CPU tests pass the kernel source's host build).  on_step(obs, action,
+    reward, next_obs, done, step_result) sees every stored transition (test hook).
+
+    episode_end: "max_steps" -- the reference's current loop (rl/training/train.py:145-169): every episode runs
+    max_steps steps without a break on done, every transition is stored, and the sticky done repeats the
+    terminal +-10 on every post-goal step.  "done" -- an episode ends at its done step (later steps of that
+    arena are neither stored nor counted): the semantics the reference's recorded runs were produced with --
+    over the 47 000 episodes of pretrained/stage_{1,2,3}/metrics/metrics.json the return never exceeds 10.0,
+    the +10 of a single goal, which the no-break loop (+10 per post-goal step) cannot produce.  A round ends
+    when every arena's episode has ended."""
     import time
     from .opponents import OpponentMix
     from .vec_env import VecHockeyEnv
@@ -455,8 +467,10 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     pool_size = cfg.self_play_pool_size if pool_size is None else pool_size
     planned = rounds * cfg.max_steps * n_arenas
     agent = TD3(cfg, device, seed, max_total_steps=planned, n_envs=n_arenas)
-    env = VecHockeyEnv(n_arenas, mode=mode, device=device, policies=("external", "external"), auto_reset=False,
-                       seed=seed)
+    own_env = env is None
+    if own_env:
+        env = VecHockeyEnv(n_arenas, mode=mode, device=device, policies=("external", "external"), auto_reset=False,
+                           seed=seed)
     mix = OpponentMix(n_arenas, curriculum, use_self_play, self_play_interval, pool_size, device, seed)
     cap = replay_capacity or max(cfg.buffer_size, n_arenas * cfg.max_steps)
     ring = (PrioritizedRing(cap, device=device, beta=cfg.beta) if cfg.prioritized_replay
@@ -472,6 +486,9 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
              "pool_size": [], "evals": [], "round_time": []}
     episodes = 0
     next_eval = cfg.eval_interval
+    if episode_end not in ("max_steps", "done"):
+        raise ValueError("episode_end must be 'max_steps' or 'done'")
+    stop_at_done = episode_end == "done"
     sync = (lambda: torch.cuda.synchronize(device)) if timing else (lambda: None)
     for rnd in range(rounds):
         sync()
@@ -480,25 +497,43 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
         if reset == "device":
             obs, obs2 = (t.clone() for t in env.reset())
         else:
-            p, _, _ = reset_params(n_arenas, seed + rnd * n_arenas + 1, mode)
+            # episode e = rnd * N + i + 1 is the train env's e-th reset: seed + e, puck side toggling per reset
+            p, _, _ = reset_params(n_arenas, seed + rnd * n_arenas + 1, mode, first_reset=rnd * n_arenas)
             env.reset_params(p)
             obs, obs2 = (t.clone() for t in env.observe())
         agent.reset_noise()
         ep_reward = torch.zeros(n_arenas, device=device)
+        alive = torch.ones(n_arenas, dtype=torch.bool, device=device)  # episode_end="done": not yet done
+        n_alive, round_steps = n_arenas, 0
         for _ in range(cfg.max_steps):
-            a = agent.act(obs)
+            a = agent.act(obs, count=n_alive)
             policy2, a2, _ = mix.select(obs2)
             act8[:, :4] = a
             if a2 is not None:
                 act8[:, 4:] = a2
             res = env.step(act8, with_agent_two=True, policy2=policy2)
             o2, r, d = res.obs.clone(), res.reward.clone(), res.done.clone()
-            ring.push(obs, a, r, o2, d)
-            mix.register_outcomes(d, r)
-            ep_reward += r
+            round_steps += n_alive
+            if stop_at_done:  # only the transitions of episodes that were still running are stored
+                idx = torch.nonzero(alive).squeeze(1)
+                ring.push(obs[idx], a[idx], r[idx], o2[idx], d[idx])
+                if on_step is not None:
+                    on_step(obs[idx], a[idx], r[idx], o2[idx], d[idx], res)
+                mix.register_outcomes(d & alive, r)
+                ep_reward += torch.where(alive, r, torch.zeros_like(r))
+                alive &= d == 0
+                n_alive = int(alive.sum())
+                if n_alive == 0:
+                    break
+            else:
+                ring.push(obs, a, r, o2, d)
+                if on_step is not None:
+                    on_step(obs, a, r, o2, d, res)
+                mix.register_outcomes(d, r)
+                ep_reward += r
             obs, obs2 = o2, res.obs2.clone()
         episodes += n_arenas
-        stats["env_steps"] += cfg.max_steps * n_arenas
+        stats["env_steps"] += round_steps
         stats["mean_reward"].append(float(ep_reward.mean().item()))
         stats["opponents"].append(mix.end_round(agent.actor, episodes=n_arenas))
         stats["pool_size"].append(len(mix.pool) if mix.pool is not None else 0)
@@ -519,7 +554,8 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
             next_eval = (episodes // cfg.eval_interval + 1) * cfg.eval_interval
         if log:
             log(rnd, stats)
-    env.close()
+    if own_env:
+        env.close()
     stats["replay_size"] = len(ring)
     stats["train_step"] = agent.train_step
     return agent, stats

@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--eval-episodes", type=int, default=100)
     ap.add_argument("--seed", type=int, default=420)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--episode-end", choices=["done", "max_steps"], default="done",
+                    help="'done': an episode ends at its goal / time limit, as in the runs behind the recorded "
+                         "metrics (their returns never exceed +10); 'max_steps': the reference's current no-break "
+                         "500-step loop (hockey_amd.td3.train docstring)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "r03", "stage1_pin.json"))
     ap.add_argument("--checkpoint", default=None, help="save the final agent (reference td3_*.pt layout) here")
     args = ap.parse_args()
@@ -47,6 +51,7 @@ def main():
     dev = "cuda:0"
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     out = {"config": vars(cfg), "arenas": n, "rounds": rounds, "episodes": rounds * n, "seed": args.seed,
+           "episode_end": args.episode_end,
            "updates_per_round": updates_for(cfg, n, cfg.max_steps), "eval_episodes": args.eval_episodes,
            "reference_wr_weak": REF_WR_WEAK, "evals": []}
     t_start = time.time()
@@ -65,7 +70,7 @@ def main():
         return rec
 
     agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, device=dev, seed=args.seed, eval_fn=eval_fn,
-                      graphs=not args.no_graphs)
+                      graphs=not args.no_graphs, episode_end=args.episode_end)
     torch.cuda.synchronize()
     wr = [e["wr_weak"] for e in out["evals"]]
     first = next((e for e in out["evals"] if e["wr_weak"] >= 0.9), None)

@@ -1,0 +1,77 @@
+"""G9: the reference's TD3 learner (rl/td3/learner.py:55-218 with rl/td3/networks.py and the agent's Adam
+settings, rl/td3/agent.py:174-182) run on a seeded batch sequence -- the golden trajectory hockey_amd.td3's
+learner is held to (tests/test_td3.py).  Runs ONLY in the build container (imports /root/reference/rl);
+commits plain arrays.
+
+Protocol: hidden size 32; initial weights = hockey_amd.td3.TD3(seed=0, h=32)'s; update k draws its batch
+(64 transitions) from torch.Generator().manual_seed(1000 + k) in the order s, a, r, s2, d and runs with
+torch.manual_seed(2000 + k) set just before it (the target-smoothing noise).  Recorded: every update's critic
+and actor loss, and the final actor / critic / target parameters (state_dict order).
+
+Usage: python tests/golden/make_td3_golden.py"""
+import copy
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(OUT))
+sys.path[:0] = [REF, os.path.join(ROOT, "hockey-env_amd")]
+
+from hockey_amd.td3 import TD3, TD3Config  # noqa: E402
+
+H, B, K = 32, 64, 30
+
+
+def batch(k):
+    g = torch.Generator().manual_seed(1000 + k)
+    s = torch.randn(B, 18, generator=g)
+    a = torch.rand(B, 4, generator=g) * 2 - 1
+    r = torch.randn(B, generator=g) * 3
+    s2 = torch.randn(B, 18, generator=g)
+    d = (torch.rand(B, generator=g) < 0.15).float()
+    return s, a, r, s2, d
+
+
+def main():
+    # the reference is imported here only: tests import this module for batch() without /root/reference
+    from rl.td3.config import TD3Config as RefConfig
+    from rl.td3.learner import TD3Learner
+    from rl.td3.networks import ActorNetwork, TwinQNetwork
+
+    init = TD3(TD3Config(), device="cpu", seed=0, h=H)
+    cfg = RefConfig()
+    pol = ActorNetwork(18, 4, h=H)
+    pol.load_state_dict(init.actor.state_dict())
+    crit = TwinQNetwork(18, 4, H, action_low=-torch.ones(4), action_high=torch.ones(4))
+    crit.load_state_dict(init.critic.state_dict())
+    tpol, tcrit = copy.deepcopy(pol), copy.deepcopy(crit)
+    for net in (tpol, tcrit):
+        for p in net.parameters():
+            p.requires_grad = False
+    copt = torch.optim.Adam(crit.parameters(), lr=cfg.lr_q, eps=1e-6, weight_decay=cfg.wd_q)
+    aopt = torch.optim.Adam(pol.parameters(), lr=cfg.lr_pol, eps=1e-6, weight_decay=cfg.wd_pol)
+
+    class _NoBuffer:  # the learner only touches the buffer under prioritized replay
+        pass
+
+    ref = TD3Learner(pol, crit, tpol, tcrit, copt, aopt, _NoBuffer(), None, cfg, "cpu", cfg.beta)
+    closs, aloss = [], []
+    for k in range(K):
+        torch.manual_seed(2000 + k)
+        al, cl = ref.update(*batch(k))
+        closs.append(cl)
+        aloss.append(np.nan if al is None else al)
+    out = {"critic_loss": np.array(closs, np.float64), "actor_loss": np.array(aloss, np.float64)}
+    for name, net in (("actor", pol), ("critic", crit), ("target_actor", tpol), ("target_critic", tcrit)):
+        for key, v in net.state_dict().items():
+            out[f"{name}/{key}"] = v.numpy()
+    np.savez(os.path.join(OUT, "g9_td3_learner.npz"), **out)
+    print("wrote g9_td3_learner.npz", len(out), "arrays")
+
+
+if __name__ == "__main__":
+    main()

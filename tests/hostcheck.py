@@ -140,3 +140,46 @@ class HostVec:
         c = np.zeros(16, np.uint64)
         self.L.hkh_counters(self.h, _p(c))
         return c
+
+
+def _observe(self):
+    o, o2 = np.zeros((self.n, 18), np.float32), np.zeros((self.n, 18), np.float32)
+    self.L.hkh_observe(self.h, _p(o), _p(o2))
+    return o, o2
+
+
+HostVec.observe = _observe
+
+
+class HostTorchEnv:
+    """VecHockeyEnv-shaped torch (CPU) view of HostVec, so hockey_amd.td3.train can run its collection loop on
+    the kernel source's host build in the CPU suite.  Every step records the actions the kernel applied."""
+
+    def __init__(self, n, **kw):
+        import torch
+
+        self.torch = torch
+        self.n = n
+        self.h = HostVec(n, **kw)
+
+    def reset(self):
+        self.h.reset()
+        return self.observe()
+
+    def reset_params(self, params, mask=None, max_t=None):
+        self.h.reset_params(np.asarray(params, np.float32), mask, max_t)
+
+    def observe(self):
+        o, o2 = self.h.observe()
+        return self.torch.from_numpy(o), self.torch.from_numpy(o2)
+
+    def step(self, actions=None, with_agent_two=False, policy2=None, **kw):
+        t = self.torch
+        a = None if actions is None else np.ascontiguousarray(t.as_tensor(actions).cpu().numpy(), np.float32)
+        p2 = None if policy2 is None else np.ascontiguousarray(t.as_tensor(policy2).cpu().numpy(), np.uint8)
+        r = self.h.step(a, with_agent_two=with_agent_two, policy2=p2, record_actions=True)
+        conv = {k: t.from_numpy(v) for k, v in vars(r).items()}
+        return SimpleNamespace(**conv)
+
+    def close(self):
+        self.h.close()

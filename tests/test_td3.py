@@ -24,6 +24,32 @@ def test_smooth_l1_matches_reference_formula():
     assert torch.equal(smooth_l1(x, y), ref)
 
 
+def test_learner_matches_reference_learner_g9():
+    """G9 (tests/golden/make_td3_golden.py): the reference's own TD3Learner (rl/td3/learner.py) run on a seeded
+    batch sequence from the same initial weights.  hockey_amd.td3 reproduces its losses and final actor /
+    critic / target parameters (float32 rounding only: Polyak averaging is fused)."""
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    from make_td3_golden import B, H, K, batch
+
+    g9 = np.load(os.path.join(GOLDEN, "g9_td3_learner.npz"))
+    agent = TD3(TD3Config(), device="cpu", seed=0, h=H)
+    for k in range(K):
+        torch.manual_seed(2000 + k)
+        al, cl = agent.update(*batch(k))
+        assert abs(float(cl) - g9["critic_loss"][k]) <= 1e-5 * max(1.0, abs(g9["critic_loss"][k])), k
+        if al is None:
+            assert np.isnan(g9["actor_loss"][k])
+        else:
+            assert abs(float(al) - g9["actor_loss"][k]) <= 1e-5 * max(1.0, abs(g9["actor_loss"][k])), k
+    for name, net in (("actor", agent.actor), ("critic", agent.critic), ("target_actor", agent.target_actor),
+                      ("target_critic", agent.target_critic)):
+        for key, v in net.state_dict().items():
+            np.testing.assert_allclose(v.numpy(), g9[f"{name}/{key}"], rtol=0, atol=1e-6, err_msg=f"{name}/{key}")
+    assert B == 64
+
+
 def test_target_and_delayed_soft_update():
     torch.manual_seed(0)
     agent = TD3(TD3Config(batch_size=8), device="cpu")
@@ -297,3 +323,57 @@ def test_c5_training_loop_65536_arenas_with_opponent_mix():
         assert abs(o["self_play"] / (steps * n) - 0.30) < 0.01
         assert abs(o["strong"] / (steps * n) - 0.70 * 0.35) < 0.01
     assert torch.isfinite(agent.actor(torch.zeros(4, 18, device="cuda:0"))).all()
+
+
+def test_collection_loop_on_host_build_stores_what_the_kernel_applied():
+    """hockey_amd.td3.train's collection on the kernel source's host build (tests/hostcheck.py): every stored
+    transition's action is the one the kernel applied to player 1 (clipped to [-1, 1]), its next obs is the
+    step's obs, the next transition starts from it, player 2 is the weak bot (stage-1 curriculum), and the
+    ring holds exactly the stored transitions."""
+    from hostcheck import HostTorchEnv
+
+    from hockey_amd.td3 import train
+
+    n, steps = 8, 40
+    env = HostTorchEnv(n, policies=("external", "external"))
+    seen = []
+
+    def on_step(obs, a, r, o2, d, res):
+        seen.append((obs.clone(), a.clone(), r.clone(), o2.clone(), d.clone(), res.actions.clone()))
+
+    cfg = TD3Config(max_steps=steps, start_steps=100, batch_size=32, use_self_play=False,
+                    curriculum_name="stage1")
+    agent, st = train(n_arenas=n, rounds=2, cfg=cfg, device="cpu", seed=3, env=env, on_step=on_step,
+                      graphs=False, updates_per_round=4)
+    assert len(seen) == 2 * steps and st["updates"] == 8 and st["replay_size"] == 2 * steps * n
+    for t, (obs, a, r, o2, d, applied) in enumerate(seen):
+        assert torch.equal(applied[:, :4], torch.clamp(a, -1, 1)), t
+        assert torch.all(applied[:, 4:7].abs().sum(1) > 0)  # the fused weak bot acts for player 2
+        if t % steps:
+            assert torch.equal(obs, seen[t - 1][3]), t  # transitions chain within an episode
+    assert st["opponents"][0] == {"strong": 0, "weak": steps * n, "self_play": 0}
+
+
+def test_episode_end_done_stores_only_running_episodes():
+    """episode_end="done": an arena's transitions stop at its done step (the last stored one carries done=1),
+    the agent's step count advances only for running episodes, and the round ends once every episode has."""
+    from hostcheck import HostTorchEnv
+
+    from hockey_amd.td3 import train
+
+    n = 8
+    env = HostTorchEnv(n, policies=("external", "external"))
+    seen = []
+    cfg = TD3Config(max_steps=400, start_steps=10 ** 9, batch_size=32, use_self_play=False, curriculum_name="stage1")
+    agent, st = train(n_arenas=n, rounds=1, cfg=cfg, device="cpu", seed=5, env=env, graphs=False,
+                      updates_per_round=0, episode_end="done",
+                      on_step=lambda o, a, r, o2, d, res: seen.append((d.clone(), res.done.clone())))
+    stored = sum(int(d.numel()) for d, _ in seen)
+    assert st["replay_size"] == stored == st["env_steps"] == agent.total_steps
+    # each stored step holds exactly the arenas not yet done; the round stops at the last done (time limit 251)
+    running = n
+    for d, full in seen:
+        assert d.numel() == running
+        running -= int(d.sum())
+    assert running == 0 and len(seen) <= 251
+    assert stored < n * len(seen) or len(seen) == 251
