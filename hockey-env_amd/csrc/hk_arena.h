@@ -473,78 +473,87 @@ HK_DEV void begin_contact(Arena &w, int p) {  // per-lane p
   }
 }
 
-// b2Contact::Update for a pair the broad phase could not reject: narrow phase, impulse carry-over,
-// wake-ups and BeginContact.
-HK_DEV void pair_update_near(Arena &w, int p) {
-  const int fA = SLDS.pairA[p], fB = SLDS.pairB[p], bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];
-  const uint32_t bit = 1u << p;
-  const int was = (w.touch & bit) != 0u;
-  w.enabled |= bit;
+// Narrow phase of pair p for the arena whose manifold records start at `man` (arena index a of n): the
+// manifold from the two fixtures' transforms, the impulse carry-over from the stored manifold (ids matched,
+// meaningful only if the pair was touching), and the whole-record write when touching.  Returns touching.
+// Reads only its arguments, the scene and the pair's own record, so any lane may run it for any arena.
+HK_DEV int narrow_phase(float *man, int64_t n, int64_t a, int p, int was, const xform &xA, const xform &xB) {
+  const int fA = SLDS.pairA[p], fB = SLDS.pairB[p], bA = SLDS.pbodyA[p];
   // the stored manifold (ids / impulses) of a touching pair is requested before the narrow phase so its
   // HBM / L2 latency overlaps the clipping arithmetic
   const int slot = SLDS.manslot[p];
+  Quad *rec = reinterpret_cast<Quad *>(man + ((int64_t)(slot < 0 ? 0 : slot) * n + a) * NMF);
   Quad o0 = Quad{0.0f, 0.0f, 0.0f, 0.0f}, o2 = o0, o3 = o0;
   if (slot >= 0 && was) {
-    const Quad *orec = man_rec(w, slot);
-    o0 = orec[0];
-    o2 = orec[2];
-    o3 = orec[3];
+    o0 = rec[0];
+    o2 = rec[2];
+    o3 = rec[3];
   }
-  int touching;
-  {
-    const xform xA = body_xf(w, bA), xB = body_xf(w, bB);
-    if (SLDS.sensor[p]) {
-      touching = test_overlap(SLDS.fx[fA], xA, SLDS.fx[fB], xB);
-    } else {
-      Manifold m;
-      if (SLDS.fx[fB].circle) {  // puck: A is a static quad or a player
-        const RFix<1> cB = load_fix<1>(SLDS.fx[fB]);
-        if (bA >= 3) collide_poly_circle(m, load_fix<kStaticVerts>(SLDS.fx[fA]), xA, cB, xB);
-        else collide_poly_circle(m, load_fix<kMaxPolyVerts>(SLDS.fx[fA]), xA, cB, xB);
-      } else {  // player B: A is a static quad or the other player
-        const RFix<kMaxPolyVerts> pB = load_fix<kMaxPolyVerts>(SLDS.fx[fB]);
-        if (bA >= 3) collide_polygons(m, load_fix<kStaticVerts>(SLDS.fx[fA]), xA, pB, xB);
-        else collide_polygons(m, load_fix<kMaxPolyVerts>(SLDS.fx[fA]), xA, pB, xB);
-      }
-      touching = m.count > 0;
-      if (touching) {
-        Quad *rec = man_rec(w, slot);
-        // match old contact ids to carry impulses (the stored manifold is meaningful only if touching)
-        int oc = 0;
-        uint32_t oid0 = 0u, oid1 = 0u;
-        float oni0 = 0.0f, oni1 = 0.0f, oti0 = 0.0f, oti1 = 0.0f;
-        if (was) {
-          oc = __float_as_int(o0.x) & 0xff;
-          oid0 = (uint32_t)__float_as_int(o2.y);
-          oid1 = (uint32_t)__float_as_int(o2.z);
-          oni0 = o3.x;
-          oti0 = o3.y;
-          oni1 = o3.z;
-          oti1 = o3.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (i < m.count) {
-            m.ni[i] = 0.0f;
-            m.ti[i] = 0.0f;
-            if (oc > 0 && oid0 == m.id[i]) { m.ni[i] = oni0; m.ti[i] = oti0; }
-            else if (oc > 1 && oid1 == m.id[i]) { m.ni[i] = oni1; m.ti[i] = oti1; }
-          }
-        }
-        // whole-record write; a one-point manifold's point-1 words are zeroed (every reader is bounded by
-        // the point count, as in Box2D)
-        const bool two = m.count > 1;
-        rec[0] = Quad{__int_as_float(m.count | (m.type << 8)), m.ln.x, m.ln.y, m.lp.x};
-        rec[1] = Quad{m.lp.y, m.pt_lp[0].x, m.pt_lp[0].y, two ? m.pt_lp[1].x : 0.0f};
-        rec[2] = Quad{two ? m.pt_lp[1].y : 0.0f, __int_as_float((int)m.id[0]), two ? __int_as_float((int)m.id[1]) : 0,
-                      0.0f};
-        rec[3] = Quad{m.ni[0], m.ti[0], two ? m.ni[1] : 0.0f, two ? m.ti[1] : 0.0f};
-      }
-      if (touching != was) { set_awake(w, bA, 1); set_awake(w, bB, 1); }
+  if (SLDS.sensor[p]) return test_overlap(SLDS.fx[fA], xA, SLDS.fx[fB], xB);
+  Manifold m;
+  if (SLDS.fx[fB].circle) {  // puck: A is a static quad or a player
+    const RFix<1> cB = load_fix<1>(SLDS.fx[fB]);
+    if (bA >= 3) collide_poly_circle(m, load_fix<kStaticVerts>(SLDS.fx[fA]), xA, cB, xB);
+    else collide_poly_circle(m, load_fix<kMaxPolyVerts>(SLDS.fx[fA]), xA, cB, xB);
+  } else {  // player B: A is a static quad or the other player
+    const RFix<kMaxPolyVerts> pB = load_fix<kMaxPolyVerts>(SLDS.fx[fB]);
+    if (bA >= 3) collide_polygons(m, load_fix<kStaticVerts>(SLDS.fx[fA]), xA, pB, xB);
+    else collide_polygons(m, load_fix<kMaxPolyVerts>(SLDS.fx[fA]), xA, pB, xB);
+  }
+  const int touching = m.count > 0;
+  if (touching) {
+    // match old contact ids to carry impulses (the stored manifold is meaningful only if touching)
+    int oc = 0;
+    uint32_t oid0 = 0u, oid1 = 0u;
+    float oni0 = 0.0f, oni1 = 0.0f, oti0 = 0.0f, oti1 = 0.0f;
+    if (was) {
+      oc = __float_as_int(o0.x) & 0xff;
+      oid0 = (uint32_t)__float_as_int(o2.y);
+      oid1 = (uint32_t)__float_as_int(o2.z);
+      oni0 = o3.x;
+      oti0 = o3.y;
+      oni1 = o3.z;
+      oti1 = o3.w;
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i < m.count) {
+        m.ni[i] = 0.0f;
+        m.ti[i] = 0.0f;
+        if (oc > 0 && oid0 == m.id[i]) { m.ni[i] = oni0; m.ti[i] = oti0; }
+        else if (oc > 1 && oid1 == m.id[i]) { m.ni[i] = oni1; m.ti[i] = oti1; }
+      }
+    }
+    // whole-record write; a one-point manifold's point-1 words are zeroed (every reader is bounded by
+    // the point count, as in Box2D)
+    const bool two = m.count > 1;
+    rec[0] = Quad{__int_as_float(m.count | (m.type << 8)), m.ln.x, m.ln.y, m.lp.x};
+    rec[1] = Quad{m.lp.y, m.pt_lp[0].x, m.pt_lp[0].y, two ? m.pt_lp[1].x : 0.0f};
+    rec[2] = Quad{two ? m.pt_lp[1].y : 0.0f, __int_as_float((int)m.id[0]), two ? __int_as_float((int)m.id[1]) : 0,
+                  0.0f};
+    rec[3] = Quad{m.ni[0], m.ti[0], two ? m.ni[1] : 0.0f, two ? m.ti[1] : 0.0f};
   }
+  return touching;
+}
+
+// b2Contact::Update bookkeeping of pair p once its narrow phase has run: enable, wake-ups on a touching
+// change (solid pairs), the touching bit and BeginContact -- the order-dependent side effects, applied by the
+// owner lane in pair order.
+HK_DEV void pair_update_apply(Arena &w, int p, int touching) {
+  const uint32_t bit = 1u << p;
+  const int was = (w.touch & bit) != 0u;
+  w.enabled |= bit;
+  if (!SLDS.sensor[p] && touching != was) { set_awake(w, SLDS.pbodyA[p], 1); set_awake(w, SLDS.pbodyB[p], 1); }
   w.touch = touching ? (w.touch | bit) : (w.touch & ~bit);
   if (!was && touching) begin_contact(w, p);
+}
+
+// b2Contact::Update for a pair the broad phase could not reject: narrow phase, impulse carry-over,
+// wake-ups and BeginContact.
+HK_DEV void pair_update_near(Arena &w, int p) {
+  const int was = (w.touch & (1u << p)) != 0u;
+  const int touching = narrow_phase(w.man, w.n, w.a, p, was, body_xf(w, SLDS.pbodyA[p]), body_xf(w, SLDS.pbodyB[p]));
+  pair_update_apply(w, p, touching);
 }
 
 // b2Contact::Update for a pair the broad phase rejects: not touching (no manifold, no BeginContact)
@@ -561,27 +570,103 @@ HK_DEV void pair_update(Arena &w, int p) {  // per-lane p (TOI events)
   else pair_update_near(w, p);
 }
 
+// The near pairs' narrow phases of the whole wave, dealt out over all its lanes (device build; every lane of
+// the wave that runs the step calls it).  Per lane, `near` holds the pairs whose narrow phase must run.  With
+// every dynamic body awake the narrow phases of one lane are independent of each other (transforms do not
+// change during Collide, wake-ups of awake bodies are no-ops, BeginContact touches no narrow-phase input), so
+// they may run anywhere and in any order: each (lane, pair) goes to an LDS work list with the pair's two body
+// transforms, a worker lane runs narrow_phase for the owner's arena (reading and writing the owner's manifold
+// record in HBM) and leaves `touching` in the owner's LDS row; the owner then applies the order-dependent
+// bookkeeping in pair order.  A lane with k near pairs no longer holds the wave for k narrow phases.
+#ifndef HK_COOP_COLLIDE  // experiment knob (A/B builds only): 0 = per-lane narrow-phase queue
+#define HK_COOP_COLLIDE 1
+#endif
+HK_DEV void collide_near_wave(Arena &w, uint32_t near) {
+#if defined(__HIP_DEVICE_COMPILE__) && HK_COOP_COLLIDE
+  float *q = w.lds + kLdsPerLane * 64;
+  const uint64_t lt = (1ull << w.lane) - 1ull;
+  const int64_t a0 = w.a - w.lane;  // arena of lane 0 of this wave
+  while (wave_any(near != 0u)) {
+    const int cnt = __popc(near);
+    int off = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const uint64_t m = __ballot((cnt >> b) & 1);
+      off += __popcll(m & lt) << b;
+      total += __popcll(m) << b;
+    }
+    uint32_t listed = 0u;
+    for (uint32_t m = near; m && off < kToiQ; m &= m - 1u, ++off) {
+      const int p = __ffs(m) - 1;
+      const xform xA = body_xf(w, SLDS.pbodyA[p]), xB = body_xf(w, SLDS.pbodyB[p]);
+      const int was = (w.touch >> p) & 1u;
+      float *it = q + off * kToiItemWords;
+      it[0] = __int_as_float(p | (w.lane << 8) | (was << 16));
+      it[1] = xA.p.x;
+      it[2] = xA.p.y;
+      it[3] = xA.q.s;
+      it[4] = xA.q.c;
+      it[5] = xB.p.x;
+      it[6] = xB.p.y;
+      it[7] = xB.q.s;
+      it[8] = xB.q.c;
+      listed |= m & (0u - m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int n = total < kToiQ ? total : kToiQ;
+    const uint64_t act = __ballot(1);  // workers: the wave's active lanes (see toi_drain_wave)
+    const int rank = __popcll(act & lt), nact = __popcll(act);
+    for (int k = rank; k < n; k += nact) {
+      const float *it = q + k * kToiItemWords;
+      const int tag = __float_as_int(it[0]), p = tag & 255, owner = (tag >> 8) & 255, was = (tag >> 16) & 1;
+      xform xA, xB;
+      xA.p = V(it[1], it[2]);
+      xA.q.s = it[3];
+      xA.q.c = it[4];
+      xB.p = V(it[5], it[6]);
+      xB.q.s = it[7];
+      xB.q.c = it[8];
+      const int touching = narrow_phase(w.man, w.n, a0 + owner, p, was, xA, xB);
+      w.lds[(kLdsToi + p) * 64 + owner] = touching ? 1.0f : 0.0f;  // the TOI cache row is free until SolveTOI
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    near &= ~listed;
+    for (uint32_t m = listed; m; m &= m - 1u) {  // pair order
+      const int p = __ffs(m) - 1;
+      pair_update_apply(w, p, LDS(w, kLdsToi + p) != 0.0f);
+    }
+  }
+#else
+  while (near) {
+    const int p = __ffs(near) - 1;
+    near &= near - 1u;
+    pair_update_near(w, p);
+  }
+#endif
+}
+
 // b2ContactManager::Collide.  With every dynamic body awake (the normal state of play: no arena-step of a
 // strong-vs-strong run has a sleeping body) the pair order only matters among pairs that can touch
-// (wake-ups are no-ops, far pairs fire no BeginContact), so the narrow phases are run from a per-lane
-// queue: every lane works through its own near pairs in order instead of the wave serialising over the
-// union of all lanes' near pairs.  A lane with a sleeping body takes Box2D's sequential loop.
+// (wake-ups are no-ops, far pairs fire no BeginContact), so the far pairs are settled first and the near
+// pairs' narrow phases are dealt out over the wave (collide_near_wave).  A lane with a sleeping body takes
+// Box2D's sequential loop afterwards.
 HK_DEV void collide(Arena &w) {
-  if (w.d.awake[0] && w.d.awake[1] && w.d.awake[2]) {
-    uint32_t near = 0u;
+  const bool fast = w.d.awake[0] && w.d.awake[1] && w.d.awake[2];
+  uint32_t near = 0u;
+  if (fast) {
     CoreBoxes cb;
     core_boxes(w, cb);
     for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
       if (pair_far_collide(w, p, &cb)) pair_update_far(w, p);
       else near |= 1u << p;
     }
-    while (near) {
-      const int p = __ffs(near) - 1;
-      near &= near - 1u;
-      pair_update_near(w, p);
-    }
-    return;
   }
+  collide_near_wave(w, near);  // every lane (a lane on the sequential path contributes worker capacity)
+  if (fast) return;
   for (int p = 0; p < NP; ++p) {
     const int bA = SC.pbodyA[p], bB = SC.pbodyB[p];
     const int activeA = bA < 3 && pick(w.d.awake, bA, 0);
@@ -835,7 +920,11 @@ HK_DEV void toi_drain_wave(Arena &w, uint32_t &pending, uint32_t &below) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int n = total < kToiQ ? total : kToiQ;
-    for (int k = w.lane; k < n; k += 64) {
+    // the workers are the wave's ACTIVE lanes (a partial last wave, or a single-arena context, has fewer
+    // than 64): active lane r takes items r, r + nact, ...
+    const uint64_t act = __ballot(1);
+    const int rank = __popcll(act & lt), nact = __popcll(act);
+    for (int k = rank; k < n; k += nact) {
       const float *it = q + k * kToiItemWords;
       const int tag = __float_as_int(it[0]), p = tag & 255, owner = tag >> 8;
       const int bA = SLDS.pbodyA[p], bB = SLDS.pbodyB[p];

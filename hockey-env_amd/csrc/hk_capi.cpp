@@ -36,7 +36,15 @@ struct Ctx {
   int device = 0;
   hk::DevState s{};
   hk::KCfg cfg{};
+  // hk_step_host staging (allocated on first use): device inputs / packed outputs and their pinned host twins
+  uint8_t *hs_dev = nullptr, *hs_pin = nullptr;
 };
+
+// hk_step_host buffer layout per context: inputs [N,8] f32 actions + [N,2] f64 increments, outputs [N] packed
+// records of HK_HOST_RECORD_BYTES (obs f32[18], obs2 f32[18], done u8 + 7 pad, record f64[16])
+constexpr size_t kHostObs = 0, kHostObs2 = 72, kHostDone = 144, kHostRec = 152;
+static_assert(kHostRec + 16 * 8 == HK_HOST_RECORD_BYTES, "hk_step_host record layout");
+size_t host_in_bytes(int64_t n) { return (size_t)n * (8 * 4 + 2 * 8); }
 
 
 int check_policy(int p) { return p >= HK_POLICY_EXTERNAL && p <= HK_POLICY_BASIC_STRONG; }
@@ -128,6 +136,8 @@ int hk_destroy(void *ctx) {
   if (c->s.ws) (void)hipFree(c->s.ws);
   if (c->s.phase) (void)hipFree(c->s.phase);
   if (c->s.counters) (void)hipFree(c->s.counters);
+  if (c->hs_dev) (void)hipFree(c->hs_dev);
+  if (c->hs_pin) (void)hipHostFree(c->hs_pin);
   delete c;
   return HK_OK;
 }
@@ -180,6 +190,47 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
 }
 
 int hk_step(void *ctx, const hk_step_io *io, void *stream) { return launch_steps("hk_step", ctx, io, 1, stream); }
+
+int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t flags, void *out, void *stream) {
+  if (!ctx || !out) return fail(HK_E_INVALID, "hk_step_host: NULL argument%s");
+  Ctx *c = (Ctx *)ctx;
+  if (c->s.n != 1) return fail(HK_E_INVALID, "hk_step_host: only single-arena contexts (n_arenas == 1)%s");
+  if (!actions && (c->cfg.policy[0] == HK_POLICY_EXTERNAL || c->cfg.policy[1] == HK_POLICY_EXTERNAL))
+    return fail(HK_E_INVALID, "hk_step_host: a player takes external actions but actions is NULL%s");
+  DeviceGuard g(c->device);
+  const int64_t n = c->s.n;
+  const size_t in_b = host_in_bytes(n), out_b = (size_t)n * HK_HOST_RECORD_BYTES;
+  hipError_t e = hipSuccess;
+  if (!c->hs_dev) {
+    if ((e = hipMalloc(&c->hs_dev, in_b + out_b)) != hipSuccess) return hipfail(e, "hk_step_host: hipMalloc");
+    if ((e = hipHostMalloc(&c->hs_pin, in_b + out_b, hipHostMallocDefault)) != hipSuccess) {
+      (void)hipFree(c->hs_dev);
+      c->hs_dev = nullptr;
+      return hipfail(e, "hk_step_host: hipHostMalloc");
+    }
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  const size_t a_b = (size_t)n * 8 * 4, inc_b = (size_t)n * 2 * 8;
+  if (actions) std::memcpy(c->hs_pin, actions, a_b);
+  if (opp_inc) std::memcpy(c->hs_pin + a_b, opp_inc, inc_b);
+  if ((actions || opp_inc) && (e = hipMemcpyAsync(c->hs_dev, c->hs_pin, in_b, hipMemcpyHostToDevice, st)) != hipSuccess)
+    return hipfail(e, "hk_step_host: H2D");
+  uint8_t *o = c->hs_dev + in_b;
+  hk::StepIO s{};
+  s.actions = actions ? (const float *)c->hs_dev : nullptr;
+  s.opp_inc = opp_inc ? (const double *)(c->hs_dev + a_b) : nullptr;
+  s.obs = (float *)(o + kHostObs);
+  s.obs2 = (float *)(o + kHostObs2);
+  s.done = o + kHostDone;
+  s.record = (double *)(o + kHostRec);
+  s.flags = flags;
+  if ((e = hk::launch_step(c->s, c->cfg, s, 1, st)) != hipSuccess) return hipfail(e, "hk_step_host: launch");
+  if ((e = hipMemcpyAsync(c->hs_pin + in_b, o, out_b, hipMemcpyDeviceToHost, st)) != hipSuccess)
+    return hipfail(e, "hk_step_host: D2H");
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return hipfail(e, "hk_step_host: sync");
+  std::memcpy(out, c->hs_pin + in_b, out_b);
+  return HK_OK;
+}
 
 int hk_rollout(void *ctx, int32_t n_steps, const hk_step_io *io, void *stream) {
   return launch_steps("hk_rollout", ctx, io, n_steps, stream);

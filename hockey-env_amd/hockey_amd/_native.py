@@ -14,6 +14,7 @@ CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 OBS_DIM, ACT_DIM, INFO_DIM, STATE_DIM, AUX_DIM, PARAM_DIM, DEBUG_DIM, NUM_COUNTERS = 18, 8, 4, 18, 5, 6, 13, 16
 RECORD_DIM = 16
+HOST_RECORD_BYTES = 280  # hk_step_host output: obs f32[18], obs2 f32[18], done u8 (+7), record f64[16]
 
 POLICY_EXTERNAL, POLICY_RANDOM, POLICY_BASIC_WEAK, POLICY_BASIC_STRONG = 0, 1, 2, 3
 STEP_SKIP_PHYSICS = 1
@@ -40,7 +41,7 @@ class StepIO(ctypes.Structure):
 
 
 EXPORTS = ["hk_last_error", "hk_version", "hk_create", "hk_destroy", "hk_num_arenas", "hk_set_policy", "hk_reset",
-           "hk_step", "hk_rollout", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_opponent_phase3",
+           "hk_step", "hk_step_host", "hk_rollout", "hk_get_state", "hk_set_state", "hk_opponent_phase", "hk_opponent_phase3",
            "hk_observe", "hk_counters",
            "hk_reset_counters",
            "hk_bytes_per_step", "hk_info"]
@@ -101,6 +102,7 @@ def lib():
     L.hk_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hk_step.argtypes = [vp, ctypes.POINTER(StepIO), vp]
     L.hk_rollout.argtypes = [vp, i32, ctypes.POINTER(StepIO), vp]
+    L.hk_step_host.argtypes = [vp, vp, vp, i32, vp, vp]
     L.hk_get_state.argtypes = [vp, vp, vp, vp]
     L.hk_set_state.argtypes = [vp, vp, vp, vp, vp]
     L.hk_observe.argtypes = [vp, vp, vp, vp]
@@ -110,7 +112,7 @@ def lib():
     L.hk_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), vp]
     L.hk_reset_counters.argtypes = [vp, vp]
     L.hk_bytes_per_step.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
-    for name in ["hk_create", "hk_destroy", "hk_set_policy", "hk_reset", "hk_step", "hk_rollout", "hk_get_state",
+    for name in ["hk_create", "hk_destroy", "hk_set_policy", "hk_reset", "hk_step", "hk_step_host", "hk_rollout", "hk_get_state",
                  "hk_set_state",
                  "hk_observe", "hk_info", "hk_opponent_phase", "hk_opponent_phase3", "hk_counters", "hk_reset_counters", "hk_bytes_per_step"]:
         getattr(L, name).restype = i32

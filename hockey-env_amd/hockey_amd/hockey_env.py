@@ -8,8 +8,9 @@ one-arena :class:`~hockey_amd.vec_env.VecHockeyEnv`; the step itself always runs
 Every value a facade returns is the kernel's: obs / obs_agent_two from hk_step / hk_observe, and info,
 info_agent_two, both rewards and the has_puck / time / done / winner fields in float64 from the step kernel's
 record (hk_step_io.record; hk_info after a reset or set_state), exactly as the reference computes them.  A
-step costs ONE host-to-device copy (action and opponent phase increment packed together), ONE kernel launch
-and ONE device-to-host copy of a packed output record, then one stream synchronisation.  The fused
+step is ONE call into the library (hk_step_host): the action and the opponent's phase increment go in through
+pinned staging, the step kernel runs, and the packed result (obs, obs2, done, the float64 record) comes back
+before the call returns.  The fused
 ``HockeyEnv_BasicOpponent`` opponent draws its phase from the global ``np.random`` exactly like the
 reference's ``BasicOpponent`` (:785, :796), so seeded reference scripts reproduce.  ``render`` is out of scope.
 """
@@ -31,8 +32,6 @@ __all__ = ["HockeyEnv", "HockeyEnv_BasicOpponent", "BasicOpponent", "PolicyOppon
 # after a reset / set_state, and _AUXI the int32 aux of hk_get_state then
 _OBS, _OBS2, _DONE, _F64, _AUXI, _REC = 0, 72, 144, 152, 280, 304
 _INFO, _INFO2, _REW, _REW2 = _F64, _F64 + 32, _F64 + 64, _F64 + 72
-# packed per-step input (one H2D copy): action f32[8], then the opponent's phase increment f64[2]
-_ACT, _INC, _IN = 0, 32, 48
 
 
 def set_state_raw(state, keep_mode=True):
@@ -65,19 +64,17 @@ class HockeyEnv:
         self.verbose = verbose
         self.seed()
         self._vec = VecHockeyEnv(1, keep_mode=keep_mode, mode=self._mode, device=device, policies=_policies)
+        # reset / set_state refresh: a device record and its pinned host twin (one transfer)
         self._rec = torch.zeros(_REC, dtype=torch.uint8, device=self._vec.device)
-        self._in = torch.zeros(_IN, dtype=torch.uint8, device=self._vec.device)
-        # pinned host staging: the per-step transfers are asynchronous copies, one stream sync per step
         self._rec_h = torch.zeros(_REC, dtype=torch.uint8, pin_memory=True)
-        self._in_h = torch.zeros(_IN, dtype=torch.uint8, pin_memory=True)
-        self._act_h = np.frombuffer(self._in_h.numpy(), np.float32, N.ACT_DIM, _ACT)
-        self._inc_h = np.frombuffer(self._in_h.numpy(), np.float64, 2, _INC)
-        base, ibase = self._rec.data_ptr(), self._in.data_ptr()
-        self._io = N.StepIO()
-        self._io.actions = ibase + _ACT
-        self._io.obs, self._io.obs2, self._io.done = base + _OBS, base + _OBS2, base + _DONE
-        self._io.record = base + _F64
-        self._inc_ptr = ibase + _INC
+        base = self._rec.data_ptr()
+        # hk_step_host: host-side in / out buffers of one step (include/hockey.h HK_HOST_RECORD_BYTES)
+        self._act_np = np.zeros(N.ACT_DIM, np.float32)
+        self._inc_np = np.zeros(2, np.float64)
+        self._out_np = np.zeros(N.HOST_RECORD_BYTES, np.uint8)
+        self._step_flags = 0  # HK_STEP_* (the golden harness sets HK_STEP_SKIP_PHYSICS)
+        self._host_ptrs = (self._act_np.ctypes.data_as(ctypes.c_void_p), self._inc_np.ctypes.data_as(ctypes.c_void_p),
+                           self._out_np.ctypes.data_as(ctypes.c_void_p))
         self._ptr = {k: ctypes.c_void_p(base + off) for k, off in
                      (("obs", _OBS), ("obs2", _OBS2), ("info", _INFO), ("info2", _INFO2), ("reward", _REW),
                       ("reward2", _REW2), ("aux", _AUXI))}
@@ -108,19 +105,22 @@ class HockeyEnv:
 
     # --------------------------------------------------------------- device record
     def _refresh(self, stepped):
-        """Copy the packed record to the host in one transfer.  After a step the kernel wrote all of it; after a
-        reset / set_state the obs, info / rewards and aux of the current state are filled in first."""
-        L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
-        p = self._ptr
-        if not stepped:
+        """Decode the packed record.  After a step hk_step_host returned it in the host buffer; after a reset /
+        set_state the obs, info / rewards and aux of the current state are computed on the device and copied to
+        the host in one transfer."""
+        if stepped:
+            b = self._out_np
+        else:
+            L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
+            p = self._ptr
             N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
             N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
             N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
-        import torch
+            import torch
 
-        self._rec_h.copy_(self._rec, non_blocking=True)
-        torch.cuda.current_stream(self._vec.device).synchronize()
-        b = self._rec_h.numpy()
+            self._rec_h.copy_(self._rec, non_blocking=True)
+            torch.cuda.current_stream(self._vec.device).synchronize()
+            b = self._rec_h.numpy()
         if stepped:
             aux = np.frombuffer(b, np.float64, 5, _F64 + 80).astype(np.int32)
         else:
@@ -156,15 +156,14 @@ class HockeyEnv:
         return self._obs_out(s["obs"]), self._get_info()
 
     def _launch_step(self, a8, opp_inc=None):
-        # the previous step ended with a stream sync, so the pinned staging buffer is free to reuse
-        self._act_h[:] = a8
-        io = self._io
-        io.opp_inc = None
+        self._act_np[:] = a8
+        act_p, inc_p, out_p = self._host_ptrs
         if opp_inc is not None:
-            self._inc_h[:] = opp_inc
-            io.opp_inc = self._inc_ptr
-        self._in.copy_(self._in_h, non_blocking=True)
-        N.check(self._vec.L.hk_step(self._vec._ctx, ctypes.byref(io), self._vec._stream()), "hk_step")
+            self._inc_np[:] = opp_inc
+        else:
+            inc_p = None
+        N.check(self._vec.L.hk_step_host(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._vec._stream()),
+                "hk_step_host")
         s = self._refresh(stepped=True)
         return self._obs_out(s["obs"]), s["reward"], s["done"], False, self._info_dict(s["info"])
 

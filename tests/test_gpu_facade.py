@@ -43,7 +43,7 @@ def test_facade_g2_step_laws_exact(golden):
         keep, mode = bool(g2["keep_mode"][i]), int(g2["mode"][i])
         if (keep, mode) not in envs:
             e = HockeyEnv(keep_mode=keep, mode=mode)
-            e._io.flags = N.STEP_SKIP_PHYSICS  # world.Step as a no-op, as in the golden harness
+            e._step_flags = N.STEP_SKIP_PHYSICS  # world.Step as a no-op, as in the golden harness
             envs[(keep, mode)] = e
         env = envs[(keep, mode)]
         env._vec.set_state(g2["state"][i][None, :], g2["aux"][i][None, :])

@@ -480,3 +480,14 @@ def test_policy2_validation_and_phase_rows():
     assert np.array_equal(ph2[: n // 2, 1:], ph0[: n // 2, 1:])  # no bot walked player 2's rows there
     assert np.all(ph2[n // 2:, 2] != ph0[n // 2:, 2]) and np.array_equal(ph2[n // 2:, 1], ph0[n // 2:, 1])
     env.close()
+
+
+@pytest.mark.parametrize("n", [1, 37, 100])
+def test_partial_wave_lockstep_vs_oracle(oracle, n):
+    """Contexts whose last wave is partial (1, 37, 100 arenas): the wave-cooperative TOI and narrow-phase
+    drains deal their work to the ACTIVE lanes only -- bit-exact against the oracle on the TOI-heavy
+    strong-vs-strong workload with device auto-reset."""
+    out = _bench_path_lockstep(oracle, n, 300, 0, ("strong", "strong"), seed=70 + n)
+    assert "field" not in out, out
+    out = _bench_path_lockstep(oracle, n, 200, 2, ("external", "weak"), seed=80 + n, external=True)
+    assert "field" not in out, out
