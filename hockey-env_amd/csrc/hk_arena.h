@@ -578,11 +578,8 @@ HK_DEV void pair_update(Arena &w, int p) {  // per-lane p (TOI events)
 // transforms, a worker lane runs narrow_phase for the owner's arena (reading and writing the owner's manifold
 // record in HBM) and leaves `touching` in the owner's LDS row; the owner then applies the order-dependent
 // bookkeeping in pair order.  A lane with k near pairs no longer holds the wave for k narrow phases.
-#ifndef HK_COOP_COLLIDE  // experiment knob (A/B builds only): 0 = per-lane narrow-phase queue
-#define HK_COOP_COLLIDE 1
-#endif
 HK_DEV void collide_near_wave(Arena &w, uint32_t near) {
-#if defined(__HIP_DEVICE_COMPILE__) && HK_COOP_COLLIDE
+#if defined(__HIP_DEVICE_COMPILE__)
   float *q = w.lds + kLdsPerLane * 64;
   const uint64_t lt = (1ull << w.lane) - 1ull;
   const int64_t a0 = w.a - w.lane;  // arena of lane 0 of this wave
@@ -640,7 +637,7 @@ HK_DEV void collide_near_wave(Arena &w, uint32_t near) {
       pair_update_apply(w, p, LDS(w, kLdsToi + p) != 0.0f);
     }
   }
-#else
+#else  // host build (one lane at a time): the lane's own queue in pair order
   while (near) {
     const int p = __ffs(near) - 1;
     near &= near - 1u;

@@ -36,8 +36,12 @@ struct Ctx {
   int device = 0;
   hk::DevState s{};
   hk::KCfg cfg{};
-  // hk_step_host staging (allocated on first use): device inputs / packed outputs and their pinned host twins
-  uint8_t *hs_dev = nullptr, *hs_pin = nullptr;
+  // hk_step_host buffer (allocated on first use): inputs and packed outputs in pinned, mapped, coherent host
+  // memory.  The step kernel reads the inputs and writes the outputs through hs_map (its device address), so a
+  // step costs one launch and one stream sync, with no copy commands.  HK_STEP_HOST_STAGED=1 selects the staged
+  // variant instead (device buffer hs_dev, one H2D and one D2H copy per step) for A/B timing.
+  uint8_t *hs_pin = nullptr, *hs_map = nullptr, *hs_dev = nullptr;
+  int hs_staged = 0;
 };
 
 // hk_step_host buffer layout per context: inputs [N,8] f32 actions + [N,2] f64 increments, outputs [N] packed
@@ -201,11 +205,16 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
   const int64_t n = c->s.n;
   const size_t in_b = host_in_bytes(n), out_b = (size_t)n * HK_HOST_RECORD_BYTES;
   hipError_t e = hipSuccess;
-  if (!c->hs_dev) {
-    if ((e = hipMalloc(&c->hs_dev, in_b + out_b)) != hipSuccess) return hipfail(e, "hk_step_host: hipMalloc");
-    if ((e = hipHostMalloc(&c->hs_pin, in_b + out_b, hipHostMallocDefault)) != hipSuccess) {
-      (void)hipFree(c->hs_dev);
-      c->hs_dev = nullptr;
+  if (!c->hs_pin) {
+    const char *v = std::getenv("HK_STEP_HOST_STAGED");
+    c->hs_staged = v && v[0] == '1';
+    if (c->hs_staged && (e = hipMalloc(&c->hs_dev, in_b + out_b)) != hipSuccess)
+      return hipfail(e, "hk_step_host: hipMalloc");
+    if ((e = hipHostMalloc(&c->hs_pin, in_b + out_b, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&c->hs_map, c->hs_pin, 0)) != hipSuccess) {
+      if (c->hs_pin) (void)hipHostFree(c->hs_pin);
+      if (c->hs_dev) (void)hipFree(c->hs_dev);
+      c->hs_pin = c->hs_dev = nullptr;
       return hipfail(e, "hk_step_host: hipHostMalloc");
     }
   }
@@ -213,19 +222,21 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
   const size_t a_b = (size_t)n * 8 * 4, inc_b = (size_t)n * 2 * 8;
   if (actions) std::memcpy(c->hs_pin, actions, a_b);
   if (opp_inc) std::memcpy(c->hs_pin + a_b, opp_inc, inc_b);
-  if ((actions || opp_inc) && (e = hipMemcpyAsync(c->hs_dev, c->hs_pin, in_b, hipMemcpyHostToDevice, st)) != hipSuccess)
+  uint8_t *dev = c->hs_staged ? c->hs_dev : c->hs_map;
+  if (c->hs_staged && (actions || opp_inc) &&
+      (e = hipMemcpyAsync(c->hs_dev, c->hs_pin, in_b, hipMemcpyHostToDevice, st)) != hipSuccess)
     return hipfail(e, "hk_step_host: H2D");
-  uint8_t *o = c->hs_dev + in_b;
+  uint8_t *o = dev + in_b;
   hk::StepIO s{};
-  s.actions = actions ? (const float *)c->hs_dev : nullptr;
-  s.opp_inc = opp_inc ? (const double *)(c->hs_dev + a_b) : nullptr;
+  s.actions = actions ? (const float *)dev : nullptr;
+  s.opp_inc = opp_inc ? (const double *)(dev + a_b) : nullptr;
   s.obs = (float *)(o + kHostObs);
   s.obs2 = (float *)(o + kHostObs2);
   s.done = o + kHostDone;
   s.record = (double *)(o + kHostRec);
   s.flags = flags;
   if ((e = hk::launch_step(c->s, c->cfg, s, 1, st)) != hipSuccess) return hipfail(e, "hk_step_host: launch");
-  if ((e = hipMemcpyAsync(c->hs_pin + in_b, o, out_b, hipMemcpyDeviceToHost, st)) != hipSuccess)
+  if (c->hs_staged && (e = hipMemcpyAsync(c->hs_pin + in_b, o, out_b, hipMemcpyDeviceToHost, st)) != hipSuccess)
     return hipfail(e, "hk_step_host: D2H");
   if ((e = hipStreamSynchronize(st)) != hipSuccess) return hipfail(e, "hk_step_host: sync");
   std::memcpy(out, c->hs_pin + in_b, out_b);

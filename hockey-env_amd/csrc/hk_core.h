@@ -142,25 +142,6 @@ HK_DEV rot rot_set(float x) {
   }
   return q;
 }
-// rot_set of two angles at once: rot_set's float operations, component by component, as packed fp32
-// (v_pk_mul_f32 / v_pk_add_f32; IEEE per component, no contraction) -- bit-identical to two rot_set calls, at
-// about half the VALU issue.  rot_set(+0) == (+0, 1), so a static body's +0 angle needs no special case.
-HK_DEV void rot_set2(float xa, float xb, rot &qa, rot &qb) {
-  const f2 x = f2{xa, xb};
-  const f2 k = x * bc(0.636619772367581343f);
-  const f2 fj = f2{rintf(k[0]), rintf(k[1])};
-  const int ja = (int)fj[0], jb = (int)fj[1];
-  const f2 r = ((x - fj * bc(1.5703125f)) - fj * bc(4.837512969970703125e-4f)) - fj * bc(7.549789954891882e-8f);
-  const f2 z = r * r;
-  const f2 sn = (((bc(-1.9515295891e-4f) * z + bc(8.3321608736e-3f)) * z - bc(1.6666654611e-1f)) * z) * r + r;
-  const f2 cs = ((((bc(2.443315711809948e-5f) * z - bc(1.388731625493765e-3f)) * z + bc(4.166664568298827e-2f)) * z) *
-                     z - bc(0.5f) * z) + bc(1.0f);
-  const int qa4 = ja & 3, qb4 = jb & 3;
-  qa.s = qa4 == 0 ? sn[0] : (qa4 == 1 ? cs[0] : (qa4 == 2 ? -sn[0] : -cs[0]));
-  qa.c = qa4 == 0 ? cs[0] : (qa4 == 1 ? -sn[0] : (qa4 == 2 ? -cs[0] : sn[0]));
-  qb.s = qb4 == 0 ? sn[1] : (qb4 == 1 ? cs[1] : (qb4 == 2 ? -sn[1] : -cs[1]));
-  qb.c = qb4 == 0 ? cs[1] : (qb4 == 1 ? -sn[1] : (qb4 == 2 ? -cs[1] : sn[1]));
-}
 HK_DEV v2 mul_rv(rot q, v2 v) { return V(q.c * v.x - q.s * v.y, q.s * v.x + q.c * v.y); }
 HK_DEV v2 mulT_rv(rot q, v2 v) { return V(q.c * v.x + q.s * v.y, -q.s * v.x + q.c * v.y); }
 HK_DEV rot mulT_rr(rot q, rot r) { rot o; o.s = q.c * r.s - q.s * r.c; o.c = q.c * r.c + q.s * r.s; return o; }

@@ -11,10 +11,6 @@
 
 namespace hk {
 
-#ifndef HK_ROT_SET2  // experiment knob (A/B builds only): 0 = scalar rot_set per body
-#define HK_ROT_SET2 1
-#endif
-
 // Host harness only (hostcheck, HK_HOST_DIAG): how often the velocity loop's island retirement and slot swaps
 // ran, so a CPU test can show that its lockstep runs exercised them.  [0] an island retired while another
 // of its lane's islands kept iterating, [1] a lane's live contacts were swapped into slots 0/1.
@@ -155,12 +151,13 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
   get_vel_a(B, bA, vA, wA);
   get_vel_b(B, bB, vB, wB);
   xform xA, xB;
-#if HK_ROT_SET2
-  rot_set2(aA, aB, xA.q, xB.q);  // a static body A reads angle +0: rot_set(+0) == (+0, 1)
-#else
-  xA.q = rot_set(aA);
+  if (bA >= 3) {  // static body: angle +0, rot_set(+0) == (+0, 1)
+    xA.q.s = 0.0f;
+    xA.q.c = 1.0f;
+  } else {
+    xA.q = rot_set(aA);
+  }
   xB.q = rot_set(aB);
-#endif
   xA.p = vsub(cA, mul_rv(xA.q, local_center(bA)));
   xB.p = vsub(cB, mul_rv(xB.q, local_center(bB)));
   // b2WorldManifold::Initialize
@@ -387,12 +384,13 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
     if (j < pcount) {
       rot qA, qB;
       // a static body stays at angle +0 (iA == 0 keeps aA bit-exact), and rot_set(+0) == (+0, 1)
-#if HK_ROT_SET2
-      rot_set2(aA, aB, qA, qB);
-#else
-      qA = rot_set(aA);
+      if (bA >= 3) {
+        qA.s = 0.0f;
+        qA.c = 1.0f;
+      } else {
+        qA = rot_set(aA);
+      }
       qB = rot_set(aB);
-#endif
       const f2 pA = cA - prv(qA, lcA), pB = cB - prv(qB, lcB);
       f2 normal, point;
       float sep;

@@ -149,27 +149,4 @@ void hkh_counters(void *h, unsigned long long *out16) {
   std::memcpy(out16, c->counters.data(), 16 * sizeof(unsigned long long));
 }
 
-// rot_set2 (packed, hk_core.h) against two rot_set calls, bit for bit: edge angles, then `n` pseudo-random
-// pairs in [-20, 20) x [-7, 7).  Returns the number of mismatching pairs.
-long long hkh_rot_set2_check(long long n) {
-  static const float edge[] = {0.0f, -0.0f, 1e-30f, -1e-30f, 0.7853981f, -0.7853981f, 1.5707963f, -1.5707963f,
-                               3.1415927f, -3.1415927f, 4.712389f, 6.2831855f, -6.2831855f, 100.0f, -100.0f, 1e4f};
-  long long bad = 0;
-  auto check = [&](float a, float b) {
-    hk::rot qa, qb;
-    hk::rot_set2(a, b, qa, qb);
-    const hk::rot ra = hk::rot_set(a), rb = hk::rot_set(b);
-    bad += __float_as_uint(qa.s) != __float_as_uint(ra.s) || __float_as_uint(qa.c) != __float_as_uint(ra.c) ||
-           __float_as_uint(qb.s) != __float_as_uint(rb.s) || __float_as_uint(qb.c) != __float_as_uint(rb.c);
-  };
-  for (float a : edge)
-    for (float b : edge) check(a, b);
-  uint64_t st = 12345u;
-  for (long long i = 0; i < n; ++i) {
-    st = st * 6364136223846793005ull + 1442695040888963407ull;
-    check((float)(int32_t)(st >> 32) * (20.0f / 2147483648.0f), (float)(int32_t)(uint32_t)st * (7.0f / 2147483648.0f));
-  }
-  return bad;
-}
-
 }  // extern "C"

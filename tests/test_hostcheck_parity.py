@@ -198,15 +198,3 @@ def test_step_record_matches_outputs_and_state(oracle):
         held += int((aux[:, 0] > 0).sum())
     assert aux[:, 3].sum() > 0 and held > 0  # goals and holds happened
 
-
-def test_packed_rot_set2_equals_rot_set():
-    """hk_core.h rot_set2 (two b2Rot::Set evaluations as packed fp32) is bit-identical to two rot_set calls
-    (edge angles and 2 M pseudo-random pairs, host build)."""
-    import ctypes
-
-    from hostcheck import lib
-
-    L = lib()
-    L.hkh_rot_set2_check.restype = ctypes.c_longlong
-    L.hkh_rot_set2_check.argtypes = [ctypes.c_longlong]
-    assert L.hkh_rot_set2_check(2_000_000) == 0
