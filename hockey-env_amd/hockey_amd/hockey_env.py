@@ -49,6 +49,22 @@ def set_state_raw(state, keep_mode=True):
     return raw, has
 
 
+class _Snap:
+    """The current state's values as the kernel returned them: obs (float64), obs2 (float32, widened when read),
+    f (float64 info[0:4], info2[4:8], reward[8], reward2[9]; after a step also has1, has2, time, done, winner in
+    [10:15]) and aux (int32 has1, has2, time, done, winner; decoded from f when first read after a step)."""
+    __slots__ = ("obs", "obs2_f32", "f", "_aux")
+
+    def __init__(self, obs, obs2_f32, f, aux=None):
+        self.obs, self.obs2_f32, self.f, self._aux = obs, obs2_f32, f, aux
+
+    @property
+    def aux(self):
+        if self._aux is None:
+            self._aux = self.f[10:15].astype(np.int32)
+        return self._aux
+
+
 class HockeyEnv:
     metadata = {"render.modes": ["human", "rgb_array"], "render_fps": FPS}
     continuous = False
@@ -72,6 +88,9 @@ class HockeyEnv:
         self._act_np = np.zeros(N.ACT_DIM, np.float32)
         self._inc_np = np.zeros(2, np.float64)
         self._out_np = np.zeros(N.HOST_RECORD_BYTES, np.uint8)
+        self._out_obs = np.frombuffer(self._out_np, np.float32, 18, _OBS)  # views into the step's out buffer
+        self._out_obs2 = np.frombuffer(self._out_np, np.float32, 18, _OBS2)
+        self._out_f = np.frombuffer(self._out_np, np.float64, 16, _F64)
         self._step_flags = 0  # HK_STEP_* (the golden harness sets HK_STEP_SKIP_PHYSICS)
         self._host_ptrs = (self._act_np.ctypes.data_as(ctypes.c_void_p), self._inc_np.ctypes.data_as(ctypes.c_void_p),
                            self._out_np.ctypes.data_as(ctypes.c_void_p))
@@ -109,30 +128,21 @@ class HockeyEnv:
         set_state the obs, info / rewards and aux of the current state are computed on the device and copied to
         the host in one transfer."""
         if stepped:
-            b = self._out_np
-        else:
-            L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
-            p = self._ptr
-            N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
-            N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
-            N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
-            import torch
+            self._snap = _Snap(self._out_obs.astype(np.float64), self._out_obs2.copy(), self._out_f.copy())
+            return self._snap
+        L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
+        p = self._ptr
+        N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
+        N.check(L.hk_info(ctx, p["info"], p["info2"], p["reward"], p["reward2"], st), "hk_info")
+        N.check(L.hk_get_state(ctx, None, p["aux"], st), "hk_get_state")
+        import torch
 
-            self._rec_h.copy_(self._rec, non_blocking=True)
-            torch.cuda.current_stream(self._vec.device).synchronize()
-            b = self._rec_h.numpy()
-        if stepped:
-            aux = np.frombuffer(b, np.float64, 5, _F64 + 80).astype(np.int32)
-        else:
-            aux = np.frombuffer(b, np.int32, 5, _AUXI).copy()
-        self._snap = {
-            "obs": np.frombuffer(b, np.float32, 18, _OBS).astype(np.float64),
-            "obs2": np.frombuffer(b, np.float32, 18, _OBS2).astype(np.float64),
-            "done": bool(b[_DONE]), "info": np.frombuffer(b, np.float64, 4, _INFO).copy(),
-            "info2": np.frombuffer(b, np.float64, 4, _INFO2).copy(),
-            "reward": float(np.frombuffer(b, np.float64, 1, _REW)[0]),
-            "reward2": float(np.frombuffer(b, np.float64, 1, _REW2)[0]),
-            "aux": aux}
+        self._rec_h.copy_(self._rec, non_blocking=True)
+        torch.cuda.current_stream(self._vec.device).synchronize()
+        b = self._rec_h.numpy()
+        self._snap = _Snap(np.frombuffer(b, np.float32, 18, _OBS).astype(np.float64),
+                           np.frombuffer(b, np.float32, 18, _OBS2).copy(),
+                           np.frombuffer(b, np.float64, 10, _F64).copy(), np.frombuffer(b, np.int32, 5, _AUXI).copy())
         return self._snap
 
     # --------------------------------------------------------------- reset / step
@@ -153,7 +163,7 @@ class HockeyEnv:
         # the mode setter changed it (hockey_env.py:357-365)
         self._vec.reset_params(params[None, :], max_t=[max_t])
         s = self._refresh(stepped=False)
-        return self._obs_out(s["obs"]), self._get_info()
+        return self._obs_out(s.obs), self._get_info()
 
     def _launch_step(self, a8, opp_inc=None):
         self._act_np[:] = a8
@@ -165,7 +175,8 @@ class HockeyEnv:
         N.check(self._vec.L.hk_step_host(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._vec._stream()),
                 "hk_step_host")
         s = self._refresh(stepped=True)
-        return self._obs_out(s["obs"]), s["reward"], s["done"], False, self._info_dict(s["info"])
+        f = s.f
+        return self._obs_out(s.obs), float(f[8]), bool(f[13]), False, self._info_dict(f[0:4])
 
     def step(self, action):
         a = np.clip(np.asarray(action, np.float64), -1, +1).astype(np.float32)  # hockey_env.py:659
@@ -178,10 +189,10 @@ class HockeyEnv:
         return o.copy() if self.keep_mode else o[:16].copy()
 
     def _get_obs(self):
-        return self._obs_out(self._snap["obs"])
+        return self._obs_out(self._snap.obs)
 
     def obs_agent_two(self):
-        return self._obs_out(self._snap["obs2"])
+        return self._obs_out(self._snap.obs2_f32.astype(np.float64))
 
     @staticmethod
     def _info_dict(v):
@@ -189,14 +200,14 @@ class HockeyEnv:
                 "reward_puck_direction": float(v[3])}
 
     def _get_info(self):
-        return self._info_dict(self._snap["info"])
+        return self._info_dict(self._snap.f[0:4])
 
     def get_info_agent_two(self):
-        return self._info_dict(self._snap["info2"])
+        return self._info_dict(self._snap.f[4:8])
 
     def _compute_reward(self):
         """hockey_env.py:518-527 from the kernel's done / winner."""
-        aux = self._snap["aux"]
+        aux = self._snap.aux
         if not aux[3]:
             return 0.0
         return 10.0 if aux[4] == 1 else (-10.0 if aux[4] != 0 else 0.0)
@@ -212,7 +223,7 @@ class HockeyEnv:
         """pybox2d setters in the reference's order; the puck's angle and angular velocity are not assigned
         (NaN = setter not called, include/hockey.h hk_set_state).  has_puck is stored as an int counter."""
         raw, has = set_state_raw(state, self.keep_mode)
-        aux = self._snap["aux"].copy()
+        aux = self._snap.aux.copy()
         if has is not None:
             aux[0], aux[1] = has
         self._vec.set_state(raw[None, :], aux[None, :])
@@ -220,23 +231,23 @@ class HockeyEnv:
 
     @property
     def time(self):
-        return int(self._snap["aux"][2])
+        return int(self._snap.aux[2])
 
     @property
     def done(self):
-        return bool(self._snap["aux"][3])
+        return bool(self._snap.aux[3])
 
     @property
     def winner(self):
-        return int(self._snap["aux"][4])
+        return int(self._snap.aux[4])
 
     @property
     def player1_has_puck(self):
-        return int(self._snap["aux"][0])
+        return int(self._snap.aux[0])
 
     @property
     def player2_has_puck(self):
-        return int(self._snap["aux"][1])
+        return int(self._snap.aux[1])
 
     def discrete_to_continous_action(self, discrete_action):
         """hockey_env.py:637-656"""

@@ -1,6 +1,6 @@
 """CPU reproduction of the reference stage-1 TD3 run, one arena at a time like rl/training/train.py, on the kernel
 source's host build (tests/hostcheck.py) -- test / diagnostic infrastructure, no GPU.  Usage: python
-scripts/td3_stage1_cpu.py <arenas> <episodes> [done|max_steps]"""
+scripts/td3_stage1_cpu.py <arenas> <episodes> [done|max_steps] [seed]"""
 import sys, os, time, json
 sys.path[:0] = ["/root/repo/tests", "/root/repo/hockey-env_amd"]
 import numpy as np, torch
@@ -28,7 +28,7 @@ def host_eval(actor, episodes=100, seed=420, weak=True):
     env.close()
     return float((winner == 1).mean())
 
-n = int(sys.argv[1]); episodes = int(sys.argv[2])
+n = int(sys.argv[1]); episodes = int(sys.argv[2]); seed = int(sys.argv[4]) if len(sys.argv) > 4 else 420
 cfg = TD3Config.from_json("/root/repo/tests/golden/stage1_config.json", eval_interval=200)
 t0 = time.time()
 def ev(agent, eps):
@@ -36,4 +36,4 @@ def ev(agent, eps):
     print(json.dumps({"episode": eps, "updates": agent.train_step, "wr_weak": wr, "t": round(time.time()-t0)}), flush=True)
     return wr
 env = HostTorchEnv(n, policies=("external", "external"))
-train(n_arenas=n, rounds=episodes // n, cfg=cfg, device="cpu", seed=420, env=env, eval_fn=ev, graphs=False, episode_end=sys.argv[3] if len(sys.argv) > 3 else "max_steps")
+train(n_arenas=n, rounds=episodes // n, cfg=cfg, device="cpu", seed=seed, env=env, eval_fn=ev, graphs=False, episode_end=sys.argv[3] if len(sys.argv) > 3 else "max_steps")
