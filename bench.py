@@ -26,6 +26,11 @@ import os
 import sys
 import time
 
+# Hardware queues per process for the `streams` side leg: S shard streams overlap only when each has a queue of
+# its own besides the default stream's (one process per configuration, profiles/r03/stream_sweep_per_process.log: S = 4
+# needs 8 queues, the box default is 4).  Set before the HIP runtime initialises; the main line uses one stream.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
 
@@ -65,7 +70,7 @@ def _args():
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU-only rehearsal of the multi-rank path (gloo, no simulation): launcher, barrier, "
                          "max-over-ranks timing and the line format; the line carries \"rehearsal\": true")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
                          "reported under 'streams'")
     return ap.parse_args()
