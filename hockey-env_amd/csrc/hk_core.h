@@ -260,8 +260,14 @@ struct PhaseT {
     (T).acc[k] += _t - (T).last;                                  \
     (T).last = _t;                                                \
   } while (0)
+#ifdef HK_T0_SPLIT  // analysis only: phase 0 split into scene copy / arena load / policy (into slots 8, 9, 10)
+#define HK_TIC_SPLIT(T, k) HK_TIC(T, k)
+#else
+#define HK_TIC_SPLIT(T, k) ((void)0)
+#endif
 #else
 struct PhaseT {};
+#define HK_TIC_SPLIT(T, k) ((void)0)
 #define HK_TIC(T, k) ((void)0)
 #define HK_FAM_T0() ((void)0)
 #define HK_FAM_ADD(T, k) ((void)0)

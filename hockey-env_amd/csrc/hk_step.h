@@ -45,16 +45,45 @@ enum { RNG_ACTION = 1, RNG_PHASE = 2, RNG_RESET = 3, RNG_PHASE0 = 4 };
 HK_DEV float &F(const DevState &s, int field, int64_t a) { return s.f[(int64_t)field * s.n + a]; }
 HK_DEV int32_t &I(const DevState &s, int field, int64_t a) { return s.i[(int64_t)field * s.n + a]; }
 
-HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, int vel_ref, float *lds, int lane) {
-  const int awake = I(s, I_AWAKE, a);
+// The HBM words one arena's step reads before it computes anything: its state, the acting BasicOpponents'
+// phases, the per-arena policy override, phase increments and external actions.  step_kernel issues these
+// loads before its scene copy, so the whole fetch costs one memory latency instead of one per dependent use.
+struct StepWords {
+  float f[NFF];
+  int32_t i[NIF];
+  double ph[3];
+  double inc[2];
+  float act[8];
+  int32_t pol2;
+};
+HK_DEV void fetch_words(StepWords &m, const DevState &s, const KCfg &cfg, const StepIO &io, int64_t a) {
+#pragma unroll
+  for (int k = 0; k < NFF; ++k) m.f[k] = F(s, k, a);
+#pragma unroll
+  for (int k = 0; k < NIF; ++k) m.i[k] = I(s, k, a);
+  // phase rows a bot may use (wave-uniform conditions; row 2 only under an override)
+  m.ph[0] = cfg.policy[0] >= 2 ? s.phase[a] : 0.0;
+  m.ph[1] = (cfg.policy[1] >= 2 || io.policy2) ? s.phase[s.n + a] : 0.0;
+  m.ph[2] = io.policy2 ? s.phase[2 * s.n + a] : 0.0;
+  m.pol2 = io.policy2 ? (int32_t)io.policy2[a] : 0;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) m.inc[p] = io.opp_inc ? io.opp_inc[a * 2 + p] : 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m.act[k] = io.actions ? io.actions[a * 8 + k] : 0.0f;
+}
+
+// the register arena from its HBM words (f: NFF floats, iw: NIF ints)
+HK_DEV void unpack_arena(Arena &w, const float *fw, const int32_t *iw, int64_t a, const DevState &s, int keep_mode,
+                         int vel_ref, float *lds, int lane) {
+  const int awake = iw[I_AWAKE];
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     const int o = b * FB;
-    w.d.px[b] = F(s, o + FB_PX, a);
-    w.d.py[b] = F(s, o + FB_PY, a);
-    w.d.cx[b] = F(s, o + FB_CX, a);
-    w.d.cy[b] = F(s, o + FB_CY, a);
-    w.d.a[b] = F(s, o + FB_A, a);
+    w.d.px[b] = fw[o + FB_PX];
+    w.d.py[b] = fw[o + FB_PY];
+    w.d.cx[b] = fw[o + FB_CX];
+    w.d.cy[b] = fw[o + FB_CY];
+    w.d.a[b] = fw[o + FB_A];
     const rot q = rot_set(w.d.a[b]);
     w.d.qs[b] = q.s;
     w.d.qc[b] = q.c;
@@ -62,10 +91,10 @@ HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, in
     w.d.c0y[b] = w.d.cy[b];
     w.d.a0[b] = w.d.a[b];
     w.d.al0[b] = 0.0f;
-    w.d.vx[b] = F(s, o + FB_VX, a);
-    w.d.vy[b] = F(s, o + FB_VY, a);
-    w.d.w[b] = F(s, o + FB_W, a);
-    w.d.sleep[b] = F(s, o + FB_SLEEP, a);
+    w.d.vx[b] = fw[o + FB_VX];
+    w.d.vy[b] = fw[o + FB_VY];
+    w.d.w[b] = fw[o + FB_W];
+    w.d.sleep[b] = fw[o + FB_SLEEP];
     w.d.awake[b] = (awake >> b) & 1;
     w.d.fx[b] = 0.0f;
     w.d.fy[b] = 0.0f;
@@ -73,16 +102,16 @@ HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, in
     w.d.ld[b] = 0.0f;
     w.d.ad[b] = 0.0f;
   }
-  w.d.fx[B_PK] = F(s, F_PFX, a);
-  w.d.fy[B_PK] = F(s, F_PFY, a);
+  w.d.fx[B_PK] = fw[F_PFX];
+  w.d.fy[B_PK] = fw[F_PFY];
   w.keep_mode = keep_mode;
   w.vel_ref = vel_ref;
-  w.has1 = I(s, I_HAS1, a);
-  w.has2 = I(s, I_HAS2, a);
-  w.time = I(s, I_TIME, a);
-  w.done = I(s, I_DONE, a);
-  w.winner = I(s, I_WINNER, a);
-  w.max_t = I(s, I_MAXT, a);
+  w.has1 = iw[I_HAS1];
+  w.has2 = iw[I_HAS2];
+  w.time = iw[I_TIME];
+  w.done = iw[I_DONE];
+  w.winner = iw[I_WINNER];
+  w.max_t = iw[I_MAXT];
   w.n_toi = 0;
   w.overflow = 0;
   w.n_big = 0;
@@ -90,8 +119,8 @@ HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, in
 #ifdef HK_PHASE_TIMERS
   w.dg_vit_isl = w.dg_vit_toi = w.dg_pit = w.dg_toi_calls = w.dg_nc_max = 0;
 #endif
-  w.touch = (uint32_t)I(s, I_TOUCH, a);
-  w.enabled = (uint32_t)I(s, I_ENABLED, a);
+  w.touch = (uint32_t)iw[I_TOUCH];
+  w.enabled = (uint32_t)iw[I_ENABLED];
   w.toiflag = w.cisl = w.bisl = 0u;
   w.man = s.man;
   w.ws = s.ws;
@@ -102,6 +131,15 @@ HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, in
 #ifdef HK_TRACE
   w.trace = nullptr;
 #endif
+}
+HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, int vel_ref, float *lds, int lane) {
+  float fw[NFF];
+  int32_t iw[NIF];
+#pragma unroll
+  for (int k = 0; k < NFF; ++k) fw[k] = F(s, k, a);
+#pragma unroll
+  for (int k = 0; k < NIF; ++k) iw[k] = I(s, k, a);
+  unpack_arena(w, fw, iw, a, s, keep_mode, vel_ref, lds, lane);
 }
 
 HK_DEV void store_arena(const Arena &w, const DevState &s, int64_t a) {
@@ -245,22 +283,26 @@ HK_DEV void reset_lane(const DevState &s, const KCfg &cfg, int64_t a, const floa
 // One HockeyEnv.step of arena a (policy actions, pre-solve laws, world.Step, outputs, then auto-reset).
 struct LaneOut { int done_edge, win1, win2, ntoi, ovf, nbig, bad_policy; };
 
+// m: the step's HBM words (fetch_words), fetched by the caller so that it can issue them early
 HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int64_t a, float *lds, int lane,
-                      PhaseT &T, LaneOut &out) {
+                      PhaseT &T, LaneOut &out, const StepWords &m) {
   Arena w;
-  load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, lds, lane);
+  unpack_arena(w, m.f, m.i, a, s, cfg.keep_mode, cfg.vel_ref, lds, lane);
   w.force_big = cfg.diag & 1;
 #ifdef HK_TRACE
   w.trace = io.debug ? io.debug + a * kTraceStride : nullptr;
 #endif
-  const uint32_t stepc = (uint32_t)I(s, I_STEP, a);
+  const uint32_t stepc = (uint32_t)m.i[I_STEP];
+  HK_TIC_SPLIT(T, 9);
   // ---- actions: external / Philox random / fused BasicOpponent ----
   float a8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a8[k] = m.act[k];  // external actions (zeros without io.actions)
   int bad_policy = 0;
   for (int p = 0; p < 2; ++p) {
     int pol = cfg.policy[p], row = p;  // row: the acting BasicOpponent's phase (DevState::phase)
     if (p == 1 && io.policy2) {
-      pol = io.policy2[a];
+      pol = m.pol2;
       row = pol == 2 ? 2 : 1;
       if (pol > 3) {  // not an HK_POLICY_*: counted (HK_CNT_BAD_POLICY), the player acts with zeros
         bad_policy = 1;
@@ -268,7 +310,8 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
       }
     }
     if (pol <= 0) {
-      for (int k = 0; k < 4; ++k) a8[4 * p + k] = (io.actions && pol == 0) ? io.actions[a * 8 + 4 * p + k] : 0.0f;
+      if (pol < 0)
+        for (int k = 0; k < 4; ++k) a8[4 * p + k] = 0.0f;
     } else if (pol == 1) {
       const int64_t ga = cfg.arena_offset + a;
       U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), stepc, RNG_ACTION + 0x10 * p);
@@ -280,13 +323,13 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
       float o[18];
       if (p == 0) observe(w, o); else observe_two(w, o);
       double inc;
-      if (io.opp_inc) inc = io.opp_inc[a * 2 + p];
+      if (io.opp_inc) inc = p == 0 ? m.inc[0] : m.inc[1];
       else {
         const int64_t ga = cfg.arena_offset + a;
         U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), stepc, RNG_PHASE + 0x10 * p);
         inc = 0.0 + (0.2 - 0.0) * u01d(r.x, r.y);
       }
-      double ph = s.phase[row * s.n + a];
+      double ph = row == 0 ? m.ph[0] : (row == 1 ? m.ph[1] : m.ph[2]);
       basic_opponent(pol == 2, w.keep_mode, ph, inc, o, &a8[4 * p]);
       s.phase[row * s.n + a] = ph;
     }
@@ -295,6 +338,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     for (int k = 0; k < 8; ++k) io.actions_out[a * 8 + k] = a8[k];
   // ---- HockeyEnv.step ----
   const int was_done = w.done;
+  HK_TIC_SPLIT(T, 10);
   HK_TIC(T, 0);
   presolve(w, a8);
   HK_TIC(T, 0);

@@ -103,7 +103,9 @@ void hkh_step(void *h, const StepIO *io) {
   for (int64_t a = 0; a < c->n; ++a) {
     PhaseT T;
     LaneOut out;
-    step_lane(c->s, c->cfg, *io, a, c->lds.data(), (int)(a & 63), T, out);
+    StepWords m;
+    fetch_words(m, c->s, c->cfg, *io, a);
+    step_lane(c->s, c->cfg, *io, a, c->lds.data(), (int)(a & 63), T, out, m);
     c->counters[0] += 1;
     c->counters[1] += out.done_edge;
     c->counters[2] += out.win1;
