@@ -6,6 +6,7 @@
 // exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -42,6 +43,7 @@ struct Ctx {
   // variant instead (device buffer hs_dev, one H2D and one D2H copy per step) for A/B timing.
   uint8_t *hs_pin = nullptr, *hs_map = nullptr, *hs_dev = nullptr;
   int hs_staged = 0;
+  uint64_t hs_seq = 0;  // hk_step_host launches so far (the completion word's expected value)
 };
 
 // hk_step_host buffer layout per context: inputs [N,8] f32 actions + [N,2] f64 increments, outputs [N] packed
@@ -49,6 +51,7 @@ struct Ctx {
 constexpr size_t kHostObs = 0, kHostObs2 = 72, kHostDone = 144, kHostRec = 152;
 static_assert(kHostRec + 16 * 8 == HK_HOST_RECORD_BYTES, "hk_step_host record layout");
 size_t host_in_bytes(int64_t n) { return (size_t)n * (8 * 4 + 2 * 8); }
+constexpr size_t kHostWordBytes = 64;  // the completion word (hk_step_host), on its own cache line
 
 
 int check_policy(int p) { return p >= HK_POLICY_EXTERNAL && p <= HK_POLICY_BASIC_STRONG; }
@@ -172,7 +175,7 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
     return fail(HK_E_INVALID, "%s: a player takes external actions but io->actions is NULL", who);
   if (io->policy2 && !io->actions)  // an override may pick HK_POLICY_EXTERNAL for any arena
     return fail(HK_E_INVALID, "%s: io->policy2 is given but io->actions is NULL", who);
-  hk::StepIO s;
+  hk::StepIO s{};
   s.actions = io->actions;
   s.opp_inc = io->opp_inc;
   s.obs = io->obs;
@@ -210,7 +213,8 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
     c->hs_staged = v && v[0] == '1';
     if (c->hs_staged && (e = hipMalloc(&c->hs_dev, in_b + out_b)) != hipSuccess)
       return hipfail(e, "hk_step_host: hipMalloc");
-    if ((e = hipHostMalloc(&c->hs_pin, in_b + out_b, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+    if ((e = hipHostMalloc(&c->hs_pin, in_b + out_b + kHostWordBytes, hipHostMallocMapped | hipHostMallocCoherent)) !=
+            hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&c->hs_map, c->hs_pin, 0)) != hipSuccess) {
       if (c->hs_pin) (void)hipHostFree(c->hs_pin);
       if (c->hs_dev) (void)hipFree(c->hs_dev);
@@ -235,10 +239,33 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
   s.done = o + kHostDone;
   s.record = (double *)(o + kHostRec);
   s.flags = flags;
+  // mapped variant: the kernel stores the launch's sequence number into a completion word in the same mapped
+  // buffer after its last output store, and the host waits on that word instead of synchronising the stream
+  volatile uint64_t *word = reinterpret_cast<volatile uint64_t *>(c->hs_pin + in_b + out_b);
+  const uint64_t seq = ++c->hs_seq;
+  if (!c->hs_staged) {
+    s.done_word = reinterpret_cast<unsigned long long *>(c->hs_map + in_b + out_b);
+    s.done_seq = seq;
+  }
   if ((e = hk::launch_step(c->s, c->cfg, s, 1, st)) != hipSuccess) return hipfail(e, "hk_step_host: launch");
-  if (c->hs_staged && (e = hipMemcpyAsync(c->hs_pin + in_b, o, out_b, hipMemcpyDeviceToHost, st)) != hipSuccess)
-    return hipfail(e, "hk_step_host: D2H");
-  if ((e = hipStreamSynchronize(st)) != hipSuccess) return hipfail(e, "hk_step_host: sync");
+  if (c->hs_staged) {
+    if ((e = hipMemcpyAsync(c->hs_pin + in_b, o, out_b, hipMemcpyDeviceToHost, st)) != hipSuccess)
+      return hipfail(e, "hk_step_host: D2H");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hipfail(e, "hk_step_host: sync");
+  } else {
+    // Spin on the word; every 4096 polls ask the stream, so a launch that fails (or never writes the word)
+    // returns its error instead of hanging the caller.
+    for (uint32_t k = 1; *word != seq; ++k) {
+      if ((k & 4095u) == 0u) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipErrorNotReady) continue;
+        if (q != hipSuccess) return hipfail(q, "hk_step_host: step kernel");
+        if (*word != seq) return fail(HK_E_DEVICE, "hk_step_host: the step finished without its completion word%s");
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
   std::memcpy(out, c->hs_pin + in_b, out_b);
   return HK_OK;
 }

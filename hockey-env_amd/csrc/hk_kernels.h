@@ -47,6 +47,10 @@ struct StepIO {
   int flags;
   const uint8_t *policy2;  // per-arena player-2 policy override (hk_step_io.policy2) or nullptr
   double *record;          // [N,16] f64 step record (hk_step_io.record) or nullptr
+  // hk_step_host only: after every output of the launch is written, arena 0's lane stores done_seq here
+  // (release at system scope), so the host can wait on this word instead of a stream synchronisation
+  unsigned long long *done_word;
+  unsigned long long done_seq;
 };
 
 hipError_t launch_init(const DevState &s, const KCfg &cfg, hipStream_t st);
