@@ -28,8 +28,10 @@ import time
 
 # Hardware queues per process for the `streams` side leg: S shard streams overlap only when each has a queue of
 # its own besides the default stream's (one process per configuration, profiles/r03/stream_sweep_per_process.log: S = 4
-# needs 8 queues, the box default is 4).  Set before the HIP runtime initialises; the main line uses one stream.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# needs 8 queues; HIP's default, and the value the GPU box exports, is 4, where S = 4 falls to 115 M).  Raised to 8
+# before the HIP runtime initialises (an exported value below 8 included); the main line uses one stream.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))

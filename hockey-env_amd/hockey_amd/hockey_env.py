@@ -65,6 +65,23 @@ class _Snap:
         return self._aux
 
 
+def _clip4_into(dst, action):
+    """dst[0:4] = float32(np.clip(np.asarray(action, np.float64)[0:4], -1, 1)) (hockey_env.py:659, 875-886),
+    without numpy temporaries for the common inputs (a float ndarray or a list).  min(max(x, -1), 1) with x
+    first returns x for NaN and keeps -0.0, as np.clip does; the float32 store rounds like astype."""
+    if isinstance(action, np.ndarray) and action.dtype.kind == "f" and action.ndim == 1 and action.shape[0] >= 4:
+        v = action[0:4].tolist()
+    elif isinstance(action, (list, tuple)) and len(action) >= 4 and all(type(x) is float for x in action[0:4]):
+        v = action[0:4]
+    else:
+        dst[0:4] = np.clip(np.asarray(action, np.float64)[0:4], -1, 1)
+        return
+    dst[0] = min(max(v[0], -1.0), 1.0)
+    dst[1] = min(max(v[1], -1.0), 1.0)
+    dst[2] = min(max(v[2], -1.0), 1.0)
+    dst[3] = min(max(v[3], -1.0), 1.0)
+
+
 class HockeyEnv:
     metadata = {"render.modes": ["human", "rgb_array"], "render_fps": FPS}
     continuous = False
@@ -166,12 +183,15 @@ class HockeyEnv:
         return self._obs_out(s.obs), self._get_info()
 
     def _launch_step(self, a8, opp_inc=None):
-        self._act_np[:] = a8
+        """a8: the 8 actions, or None when the caller wrote them into _act_np; opp_inc: the two phase increments,
+        True when the caller wrote them into _inc_np, or None (the kernel draws its own)."""
+        if a8 is not None:
+            self._act_np[:] = a8
         act_p, inc_p, out_p = self._host_ptrs
-        if opp_inc is not None:
-            self._inc_np[:] = opp_inc
-        else:
+        if opp_inc is None:
             inc_p = None
+        elif opp_inc is not True:
+            self._inc_np[:] = opp_inc
         N.check(self._vec.L.hk_step_host(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._vec._stream()),
                 "hk_step_host")
         s = self._refresh(stepped=True)
@@ -326,11 +346,14 @@ class HockeyEnv_BasicOpponent(HockeyEnv):
         self._vec.opponent_phase(np.array([[0.0, self.opponent.phase]]))
 
     def step(self, action):
-        inc = np.random.uniform(0, 0.2)  # the draw opponent.act(obs_agent_two()) makes (hockey_env.py:796)
-        self.opponent.phase += inc       # host mirror of the kernel's phase
-        a = np.zeros(8, np.float32)
-        a[0:4] = np.clip(np.asarray(action, np.float64)[0:4], -1, 1).astype(np.float32)
-        return self._launch_step(a, opp_inc=np.array([0.0, inc]))
+        # the draw opponent.act(obs_agent_two()) makes (hockey_env.py:796): RandomState.uniform(0, 0.2) is
+        # 0.0 + (0.2 - 0.0) * random_sample(), the same double as 0.2 * random() from the same global stream
+        inc = 0.2 * np.random.random()
+        self.opponent.phase += inc  # host mirror of the kernel's phase
+        _clip4_into(self._act_np, action)
+        self._act_np[4:8] = 0.0
+        self._inc_np[1] = inc
+        return self._launch_step(None, opp_inc=True)
 
 
 class PolicyOpponent:

@@ -100,3 +100,35 @@ def test_source_hash_matches_makefile_recipe():
     out = subprocess.check_output(f"cat {' '.join(N.HASH_SOURCES)} | sha256sum | cut -c1-12", shell=True,
                                   cwd=N.CSRC, text=True).strip()
     assert out == N.source_hash()
+
+
+def test_facade_action_staging_matches_numpy_clip():
+    """hockey_env._clip4_into (the facade's per-step action staging) stores exactly
+    float32(np.clip(np.asarray(action, float64)[0:4], -1, 1)) (hockey_env.py:659, 875-886) for every input kind,
+    including NaN, infinities, -0.0 and values that round across +-1 in float32."""
+    import numpy as np
+
+    from hockey_amd.hockey_env import _clip4_into
+
+    rng = np.random.default_rng(0)
+    cases = [rng.uniform(-3, 3, 4).astype(np.float32), rng.uniform(-3, 3, 8), rng.uniform(-1, 1, 6).astype(np.float16),
+             [0.5, -2.0, float("nan"), -0.0], np.array([np.inf, -np.inf, -0.0, 0.99999999], np.float64),
+             (1.0000001, -1.0000001, 0.3, 0.2), [1, 2, 3, 4], np.array([1, 2, -3, 0], np.int64),
+             np.array([[0.1, 0.2, 0.3, 0.4]]).reshape(4)]
+    for c in cases:
+        got = np.zeros(8, np.float32)
+        _clip4_into(got, c)
+        want = np.clip(np.asarray(c, np.float64)[0:4], -1, 1).astype(np.float32)
+        assert got[:4].view(np.uint32).tolist() == want.view(np.uint32).tolist(), (c, got, want)
+
+
+def test_facade_phase_increment_is_the_reference_draw():
+    """HockeyEnv_BasicOpponent.step draws 0.2 * np.random.random(): the same doubles, from the same global stream,
+    as the reference's np.random.uniform(0, 0.2) (hockey_env.py:796)."""
+    import numpy as np
+
+    np.random.seed(1234)
+    want = [np.random.uniform(0, 0.2) for _ in range(20000)]
+    np.random.seed(1234)
+    got = [0.2 * np.random.random() for _ in range(20000)]
+    assert np.array(got).view(np.uint64).tolist() == np.array(want).view(np.uint64).tolist()
