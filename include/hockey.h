@@ -142,8 +142,8 @@ int hk_step(void *ctx, const hk_step_io *io, void *stream);
 
 /* HockeyEnv.step of a SINGLE-arena context with host buffers: the reference's deployment shape (one env, numpy
  * in and out, hockey_env.py:658-695) in one call -- the action (and BasicOpponent phase increments) are staged
- * through pinned memory, the step kernel runs, and the packed result returns to `out` before the call
- * returns (it synchronises `stream`).  actions: host [1,8] f32 (NULL if no player is external); opp_inc: host
+ * through pinned memory, the step kernel runs on `stream`, and the packed result returns to `out` before the
+ * call returns (the host waits on a completion word the kernel stores after its last output, not on the stream).  actions: host [1,8] f32 (NULL if no player is external); opp_inc: host
  * [1,2] f64 or NULL; flags: HK_STEP_* (as hk_step_io.flags); out: host buffer of HK_HOST_RECORD_BYTES = obs f32[18] @0, obs2 f32[18] @72, done u8 @144,
  * hk_step_io.record f64[16] @152.  HK_E_INVALID for a context with more than one arena. */
 #define HK_HOST_RECORD_BYTES 280

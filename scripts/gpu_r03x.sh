@@ -1,6 +1,6 @@
 #!/bin/bash
 # r03x: final validation at the round's head: the full GPU suite, __graft_entry__.smoke(), and the driver's bench
-# command.  Stops at the first failure.
+# command, then the round evidence (scripts/profile_round.sh).  Stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -12,3 +12,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 $O/smoke.log
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/driver_cmd.log 2>&1 || { tail -5 $O/driver_cmd.log; exit 1; }
 grep -o '"value": [0-9.e+]*\|"counters_stale": [a-z]*\|"streams": {[^}]*}' $O/driver_cmd.log | head -6
+# round evidence at this head (counters stamped with the library hash)
+TAG=r03x ./scripts/profile_round.sh
