@@ -68,10 +68,18 @@ class TwinQ(torch.nn.Module):
         self.q1 = _QNet(n_obs + n_act, h)
         self.q2 = _QNet(n_obs + n_act, h)
 
-    def forward(self, state, action):
+    def _input(self, state, action):
         action = ((action - self.action_low) / self.action_range) * 2 - 1.0  # TwinQNetwork._unscale_action
-        x = torch.cat([state, action], dim=-1)
+        return torch.cat([state, action], dim=-1)
+
+    def forward(self, state, action):
+        x = self._input(state, action)
         return self.q1(x), self.q2(x)
+
+    def q1_only(self, state, action):
+        """The first head alone: the actor update uses only q1 (learner.py update_actor), the same values as
+        forward()[0] without the second head's forward."""
+        return self.q1(self._input(state, action))
 
 
 def smooth_l1(x, y, weights=None):
@@ -303,7 +311,7 @@ class TD3:
         actor_loss = None
         if train_actor:
             self.opt_actor.zero_grad(set_to_none=True)
-            q, _ = self.critic(s, self.actor(s))
+            q = self.critic.q1_only(s, self.actor(s))
             actor_loss = -q.mean()
             actor_loss.backward(inputs=list(self.actor.parameters()))  # the actor's gradients only
             self.opt_actor.step()
