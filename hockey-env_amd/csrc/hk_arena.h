@@ -1008,7 +1008,22 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
         elig |= settled;
         w.toiflag |= settled;
         below &= ~settled;
-        todo = kToiPairs & w.enabled & ~settled;
+        // The rest of the first pass has no order-dependent side effect either, so it runs as a uniform loop
+        // over the compile-time TOI pair table (scene data as literals, per-lane predicates) instead of each
+        // lane walking its own pairs through LDS lookups: the same flags and far tests, so the same queue.
+        const uint32_t open = kToiPairs & w.enabled & ~settled;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          if (!((kToiPairs >> p) & 1u)) continue;
+          const uint32_t bit = 1u << p;
+          const bool live = (open & bit) && w.d.awake[SC.pbodyB[p]];
+          elig |= live ? bit : 0u;
+          const bool far = live && pair_far_toi(w, p, cb, SC);
+          below &= far ? ~bit : ~0u;
+          pending |= (live && !far) ? bit : 0u;
+        }
+        w.toiflag |= elig;
+        todo = 0u;
       } else {
         // Later passes: an event re-enables TOI only on the moved dynamic body's contacts (their flags were
         // cleared).  Every other pair keeps its eligibility and cached alpha (cached pairs are eligible;
