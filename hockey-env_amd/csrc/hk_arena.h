@@ -657,7 +657,8 @@ HK_DEV void collide(Arena &w) {
   if (fast) {
     CoreBoxes cb;
     core_boxes(w, cb);
-    for (int p = 0; p < NP; ++p) {  // uniform loop: scene data through scalar loads
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {  // uniform loop, unrolled: the scene data are literals
       if (pair_far_collide(w, p, &cb)) pair_update_far(w, p);
       else near |= 1u << p;
     }
@@ -1081,7 +1082,7 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     const Sweep backA = body_sweep(w, bA), backB = body_sweep(w, bB);
     body_advance(w, bA, minAlpha);
     body_advance(w, bB, minAlpha);
-    pair_update(w, minc);
+    pair_update_near(w, minc);  // the broad-phase shortcut only ever skips narrow phases that find no contact
     HK_TIC(T, 8);  // diagnostics: TOI event advance + contact update
     w.toiflag &= ~mbit;
     const float cnt = LDS(w, kLdsCnt + minc) + 1.0f;
@@ -1103,17 +1104,33 @@ HK_DEV void solve_toi(Arena &w, float dt, PhaseT &T) {
     w.cisl |= mbit;
     uint32_t extra = 0u;  // other island contacts, added in B's (ascending) edge order
     int nc = 1;
-    uint32_t m = pick(kEdgeMask, bB, 0u) & ~kSensorMask;
+    // B's contacts with static bodies (its TOI pairs) not yet in the island.  Their broad-phase tests read only
+    // B's advanced pose and the scene, so they run first as a uniform loop over the compile-time pair table; a
+    // rejected pair's b2Contact::Update (not touching: enabled, touching bit, wake-ups of awake bodies) changes
+    // only its own bits, so it commutes with the other updates, and its tentative advance of the static body is
+    // undone in the per-lane walk anyway.  The remaining (near) pairs keep the walk in edge order.
+    const uint32_t cand = pick(kEdgeMask, bB, 0u) & kToiPairs & ~w.cisl;
+    uint32_t m = 0u;
+    {
+      CoreBoxes cbe;
+      core_boxes(w, cbe);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        if (!((kToiPairs >> p) & 1u)) continue;
+        const uint32_t bit = 1u << p;
+        if (!(cand & bit)) continue;
+        if (pair_far_collide(w, p, &cbe, SC)) pair_update_far(w, p, SC);
+        else m |= bit;
+      }
+    }
     while (m) {
       const int e = __ffs(m) - 1;
       m &= m - 1u;
       const uint32_t ebit = 1u << e;
-      if (w.cisl & ebit) continue;
-      const int other = SLDS.pbodyA[e] == bB ? SLDS.pbodyB[e] : SLDS.pbodyA[e];
-      if (other < 3) continue;  // only static bodies join a TOI island
+      const int other = SLDS.pbodyA[e];  // the static body of a TOI pair
       const Sweep backup = body_sweep(w, other);
       if (!((w.bisl >> other) & 1u)) body_advance(w, other, minAlpha);
-      pair_update(w, e);
+      pair_update_near(w, e);
       if (!(w.enabled & ebit) || !(w.touch & ebit)) {
         body_set_sweep(w, other, backup);
         continue;

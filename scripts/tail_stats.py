@@ -89,3 +89,11 @@ fam = D[:, ::64, 21:24]
 sf = fam[np.arange(steps), wave.argmax(1)]
 print("velocity families (general / two / one), cycles: mean wave", fam.mean((0, 1)).round(0).tolist(),
       " slowest wave", sf.mean(0).round(0).tolist())
+# TOI events seen from the lanes that had them: each lane's timers hold its own event phases (lane 0's slot 5
+# "toi-min" also absorbs the events of other lanes, which it waits out exec-masked)
+ev = D[:, :, 1] >= 1
+if ev.any():
+    E = D[:, :, 8:21][ev]
+    print(f"lanes with >= 1 TOI event: {ev.mean() * 100:.2f}% of lane-steps; their own phase cycles (mean):")
+    for k in (5, 6, 7, 8, 9, 10, 11):
+        print(f"  {PH[k]:22s} {E[:, k].mean():10.0f}")
