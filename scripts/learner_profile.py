@@ -12,6 +12,8 @@ import torch  # noqa: E402
 
 from hockey_amd.td3 import TD3, Learner, ReplayRing, TD3Config  # noqa: E402
 
+if os.environ.get("HK_BLAS"):  # "cublas" (rocBLAS on ROCm) or "cublaslt" (hipBLASLt, torch's default here)
+    torch.backends.cuda.preferred_blas_library(os.environ["HK_BLAS"])
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 dev = "cuda:0"
@@ -22,7 +24,7 @@ n = 1 << 20
 ring.push(torch.randn(n, 18, device=dev, generator=g), torch.rand(n, 4, device=dev, generator=g) * 2 - 1,
           torch.randn(n, device=dev, generator=g), torch.randn(n, 18, device=dev, generator=g),
           (torch.rand(n, device=dev, generator=g) < 0.01).float())
-out = {"batch": B, "updates": K}
+out = {"batch": B, "updates": K, "blas": str(torch.backends.cuda.preferred_blas_library())}
 for graphs in (False, True):
     L = Learner(agent, ring, B, graphs=graphs)
     L.run(20)
