@@ -26,12 +26,16 @@ import os
 import sys
 import time
 
-# Hardware queues per process for the `streams` side leg: S shard streams overlap only when each has a queue of
-# its own besides the default stream's (one process per configuration, profiles/r03/stream_sweep_per_process.log: S = 4
-# needs 8 queues; HIP's default, and the value the GPU box exports, is 4, where S = 4 falls to 115 M).  Raised to 8
-# before the HIP runtime initialises (an exported value below 8 included); the main line uses one stream.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# Hardware queues per process (HIP reads GPU_MAX_HW_QUEUES when its runtime starts; its default, and the value the
+# GPU box exports, is 4).  The `streams` side leg overlaps S shard streams only while each has a queue of its own
+# besides the default stream's (S < queues; profiles/r03/stream_sweep_per_process.log), so it runs
+# S = min(--streams, queues - 1) and records the queue count it ran under.  The bench never changes the variable.
+def hw_queues():
+    try:
+        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "") or 4))
+    except ValueError:
+        return 4
+
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
@@ -73,8 +77,12 @@ def _args():
                     help="CPU-only rehearsal of the multi-rank path (gloo, no simulation): launcher, barrier, "
                          "max-over-ranks timing and the line format; the line carries \"rehearsal\": true")
     ap.add_argument("--streams", type=int, default=4,
-                    help="also time the same arenas as this many shards stepped on as many HIP streams (0 = skip); "
-                         "reported under 'streams'")
+                    help="also time the same arenas as up to this many shards stepped on as many HIP streams, at most "
+                         "GPU_MAX_HW_QUEUES - 1 (0 = skip); reported under 'streams'")
+    ap.add_argument("--rank-timeout", type=float, default=1200.0,
+                    help="--gpus N launcher: wall-clock seconds after which ranks still running are killed and the "
+                         "launch fails")
+    ap.add_argument("--rehearse-hang-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher test hook
     return ap.parse_args()
 
 
@@ -203,8 +211,9 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
     step, but one shard's slowest wave no longer idles the SIMDs the other shards' steps can use."""
     from hockey_amd.vec_env import VecHockeyEnv
 
-    S, n = args.streams, args.arenas
-    if n % S:
+    q = hw_queues()
+    S, n = min(args.streams, q - 1), args.arenas
+    if S < 2 or n % S:
         return None
     m = n // S
     envs, ios, streams = [], [], []
@@ -244,7 +253,7 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
         elapsed = float(t.item())
     for e in envs:
         e.close()
-    return {"streams": S, "arenas_per_stream": m, "value": n * world * args.steps / elapsed,
+    return {"streams": S, "arenas_per_stream": m, "hw_queues": q, "value": n * world * args.steps / elapsed,
             "unit": "env-steps/s", "ms_per_step": elapsed / args.steps * 1e3}
 
 
@@ -353,12 +362,28 @@ def launch_ranks(args):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
-    if bad:
-        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr, flush=True)
-        return 1
-    return 0
+    # wait for every rank under one wall-clock limit; a rank that fails or a rank still running at the limit ends
+    # the launch, and the ranks still running (likely waiting on the lost one in a collective) are killed
+    deadline = time.monotonic() + args.rank_timeout
+    why = None
+    while why is None:
+        rcs = [p.poll() for p in procs]
+        bad = [(r, rc) for r, rc in enumerate(rcs) if rc not in (None, 0)]
+        if bad:
+            why = f"rank(s) failed: {bad}"
+        elif all(rc == 0 for rc in rcs):
+            return 0
+        elif time.monotonic() > deadline:
+            why = f"rank(s) {[r for r, rc in enumerate(rcs) if rc is None]} still running after {args.rank_timeout:g} s"
+        else:
+            time.sleep(0.1)
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+    for p in procs:
+        p.wait()
+    print(f"bench.py: {why}", file=sys.stderr, flush=True)
+    return 1
 
 
 class RehearsalEnv:
@@ -445,6 +470,8 @@ def main():
         io.info = env.info_buf.data_ptr()
     else:
         env = RehearsalEnv(n)
+        if rank == args.rehearse_hang_rank:
+            time.sleep(3600)  # launcher test hook: a rank that never reaches the barrier
 
     preroll(env, args.preroll, N)
     for _ in range(args.warmup):

@@ -51,7 +51,9 @@ struct Ctx {
 constexpr size_t kHostObs = 0, kHostObs2 = 72, kHostDone = 144, kHostRec = 152;
 static_assert(kHostRec + 16 * 8 == HK_HOST_RECORD_BYTES, "hk_step_host record layout");
 size_t host_in_bytes(int64_t n) { return (size_t)n * (8 * 4 + 2 * 8); }
-constexpr size_t kHostWordBytes = 64;  // the completion word (hk_step_host), on its own cache line
+constexpr size_t kHostWordBytes = 64;  // the completion word (hk_step_host), on its own 64-B line
+// offset of the completion word in the pinned buffer: the inputs and the records, rounded up to a 64-B line
+size_t host_word_off(int64_t n) { return (host_in_bytes(n) + (size_t)n * HK_HOST_RECORD_BYTES + 63) & ~(size_t)63; }
 
 
 int check_policy(int p) { return p >= HK_POLICY_EXTERNAL && p <= HK_POLICY_BASIC_STRONG; }
@@ -213,14 +215,18 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
     c->hs_staged = v && v[0] == '1';
     if (c->hs_staged && (e = hipMalloc(&c->hs_dev, in_b + out_b)) != hipSuccess)
       return hipfail(e, "hk_step_host: hipMalloc");
-    if ((e = hipHostMalloc(&c->hs_pin, in_b + out_b + kHostWordBytes, hipHostMallocMapped | hipHostMallocCoherent)) !=
-            hipSuccess ||
+    const size_t pin_b = host_word_off(n) + kHostWordBytes;
+    if ((e = hipHostMalloc(&c->hs_pin, pin_b, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&c->hs_map, c->hs_pin, 0)) != hipSuccess) {
       if (c->hs_pin) (void)hipHostFree(c->hs_pin);
       if (c->hs_dev) (void)hipFree(c->hs_dev);
       c->hs_pin = c->hs_dev = nullptr;
       return hipfail(e, "hk_step_host: hipHostMalloc");
     }
+    // pinned memory is not zeroed and small blocks are recycled: a stale completion word equal to the first
+    // expected sequence number (1) would end the first wait before the kernel ran
+    std::memset(c->hs_pin, 0, pin_b);
+    c->hs_seq = 0;
   }
   const hipStream_t st = (hipStream_t)stream;
   const size_t a_b = (size_t)n * 8 * 4, inc_b = (size_t)n * 2 * 8;
@@ -241,10 +247,10 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
   s.flags = flags;
   // mapped variant: the kernel stores the launch's sequence number into a completion word in the same mapped
   // buffer after its last output store, and the host waits on that word instead of synchronising the stream
-  volatile uint64_t *word = reinterpret_cast<volatile uint64_t *>(c->hs_pin + in_b + out_b);
+  volatile uint64_t *word = reinterpret_cast<volatile uint64_t *>(c->hs_pin + host_word_off(n));
   const uint64_t seq = ++c->hs_seq;
   if (!c->hs_staged) {
-    s.done_word = reinterpret_cast<unsigned long long *>(c->hs_map + in_b + out_b);
+    s.done_word = reinterpret_cast<unsigned long long *>(c->hs_map + host_word_off(n));
     s.done_seq = seq;
   }
   if ((e = hk::launch_step(c->s, c->cfg, s, 1, st)) != hipSuccess) return hipfail(e, "hk_step_host: launch");

@@ -250,7 +250,7 @@ HK_DEV bool wave_any(bool p) { return p; }
 // Diagnostic build only (make TIMERS=1): per-phase shader-clock accounting; compiled out otherwise.
 #ifdef HK_PHASE_TIMERS
 struct PhaseT {
-  unsigned long long last, acc[13], fam[3];  // fam: velocity-loop cycles in the general / two / one families
+  unsigned long long last, acc[16], fam[3];  // acc: phases 0-12 + the phase-0 split 13-15; fam: velocity-loop cycles in the general / two / one families
 };
 #define HK_FAM_T0() const unsigned long long _ft0 = __builtin_amdgcn_s_memtime()
 #define HK_FAM_ADD(T, k) ((T).fam[k] += __builtin_amdgcn_s_memtime() - _ft0)
@@ -260,7 +260,7 @@ struct PhaseT {
     (T).acc[k] += _t - (T).last;                                  \
     (T).last = _t;                                                \
   } while (0)
-#ifdef HK_T0_SPLIT  // analysis only: phase 0 split into scene copy / arena load / policy (into slots 8, 9, 10)
+#ifdef HK_T0_SPLIT  // analysis only: phase 0 split into scene copy / arena load / policy (own slots 13, 14, 15)
 #define HK_TIC_SPLIT(T, k) HK_TIC(T, k)
 #else
 #define HK_TIC_SPLIT(T, k) ((void)0)

@@ -9,7 +9,8 @@
 //                               enabled mask, one_starts, episode and step counters
 //   man[NSOLID][N][NMF]  float  Box2D manifold record (64 B) of every solid pair (read/written in place,
 //                               touching only; hk_arena.h man_rec)
-//   phase[2][N]          double BasicOpponent phases (global np.random stream -> per-arena Philox)
+//   phase[3][N]          double BasicOpponent phases: player 1, player 2, player 2's weak bot under a per-arena
+//                               override (global np.random stream -> per-arena Philox)
 #pragma once
 #include "hk_arena.h"
 
@@ -293,7 +294,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
   w.trace = io.debug ? io.debug + a * kTraceStride : nullptr;
 #endif
   const uint32_t stepc = (uint32_t)m.i[I_STEP];
-  HK_TIC_SPLIT(T, 9);
+  HK_TIC_SPLIT(T, 14);
   // ---- actions: external / Philox random / fused BasicOpponent ----
   float a8[8];
 #pragma unroll
@@ -338,7 +339,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     for (int k = 0; k < 8; ++k) io.actions_out[a * 8 + k] = a8[k];
   // ---- HockeyEnv.step ----
   const int was_done = w.done;
-  HK_TIC_SPLIT(T, 10);
+  HK_TIC_SPLIT(T, 15);
   HK_TIC(T, 0);
   presolve(w, a8);
   HK_TIC(T, 0);

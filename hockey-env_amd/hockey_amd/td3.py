@@ -156,7 +156,7 @@ class ReplayRing:
         self.r = torch.zeros(self.cap, device=d)
         self.s2 = torch.zeros((self.cap, n_obs), device=d)
         self.d = torch.zeros(self.cap, device=d)
-        self.size_t = torch.zeros((), dtype=torch.float32, device=d)
+        self.size_t = torch.zeros((), dtype=torch.int64, device=d)  # fill level, exact at any capacity
 
     def _slots(self, n):
         """Ring slots of the next n pushes, as one or two contiguous ranges."""
@@ -180,13 +180,16 @@ class ReplayRing:
             self.d[lo:hi] = d[off:off + m].float()
         self.pos = (self.pos + n) % self.cap
         self.size = min(self.size + n, self.cap)
-        self.size_t.fill_(float(self.size))
+        self.size_t.fill_(self.size)
 
     def _before_push(self, n):
         pass
 
     def sample_indices(self, batch):
-        return (torch.rand(batch, device=self.device) * self.size_t).long()
+        # float64 uniforms: float32's 24-bit mantissa cannot reach every slot of a ring past 2^24 transitions
+        # (C5 fills 32.8 M) and skews the draw well below that; the reference draws in float64 too
+        u = torch.rand(batch, device=self.device, dtype=torch.float64)
+        return torch.minimum((u * self.size_t).long(), self.size_t - 1)
 
     def sample(self, batch):
         """(s, a, r, s2, d, importance weights or None)."""
@@ -231,7 +234,7 @@ class PrioritizedRing(ReplayRing):
             self.w[lo:hi] = wmax
 
     def sample_indices(self, batch):
-        valid = self._slot.float() < self.size_t
+        valid = self._slot < self.size_t
         w = torch.nan_to_num(self.w, nan=0.0, posinf=0.0, neginf=0.0).clamp_min(1e-6) * valid
         cdf = torch.cumsum(w.double(), 0)
         u = torch.rand(batch, device=self.device, dtype=torch.float64) * cdf[-1]

@@ -101,3 +101,16 @@ def test_bench_failed_rank_fails_the_launch():
     rc, lines, err = _bench(["--gpus", "2", "--rehearse", "--steps", "2", "--warmup", "0", "--preroll", "0",
                              "--arenas", "0"])
     assert rc != 0
+
+
+def test_bench_hung_rank_times_out_and_fails_the_launch():
+    """A rank that never reaches the barrier: the launcher kills the ranks still running at --rank-timeout and
+    exits non-zero, instead of waiting forever."""
+    import time
+
+    t0 = time.monotonic()
+    rc, lines, err = _bench(["--gpus", "2", "--rehearse", "--steps", "2", "--warmup", "0", "--preroll", "0",
+                             "--arenas", "64", "--rank-timeout", "20", "--rehearse-hang-rank", "1"])
+    assert rc != 0 and not lines
+    assert "still running after 20 s" in err, err[-2000:]
+    assert time.monotonic() - t0 < 120

@@ -264,6 +264,32 @@ def test_hockey_one_seeded_run_vs_oracle(oracle):
     env.close()
 
 
+@pytest.mark.parametrize("staged", ["0", "1"])
+def test_step_host_on_fresh_contexts_equals_hk_step(monkeypatch, staged):
+    """hk_step_host (the facade's one-call step: mapped completion word, or HK_STEP_HOST_STAGED=1 copies) on
+    freshly created and destroyed single-arena contexts -- recycled pinned blocks included -- returns exactly what
+    hk_step returns on a twin context built the same way: obs, obs2, done and the float64 step record, from the
+    very first step on."""
+    from hockey_amd.hockey_env import HockeyEnv
+
+    monkeypatch.setenv("HK_STEP_HOST_STAGED", staged)
+    rng = np.random.default_rng(int(staged))
+    for k in range(6):
+        host, twin = HockeyEnv(), HockeyEnv()
+        host.reset(seed=100 + k)
+        twin.reset(seed=100 + k)
+        for t in range(1 + k):
+            a = rng.uniform(-1, 1, 8).astype(np.float32)
+            obs, r, d, _, info = host.step(a)
+            res = twin._vec.step(a[None, :], with_agent_two=True, record=True)
+            assert np.array_equal(obs, _np(res.obs)[0].astype(np.float64)), (k, t)
+            assert np.array_equal(host.obs_agent_two(), _np(res.obs2)[0].astype(np.float64)), (k, t)
+            assert bool(d) == bool(_np(res.done)[0]), (k, t)
+            assert np.array_equal(host._out_f, _np(res.record)[0]), (k, t)
+        host.close()
+        twin.close()
+
+
 # ------------------------------------------------------------------------------------------------ behaviour
 def test_stage3_actor_reproduces_recorded_win_rates(golden):
     """The reference's stage-3 best actor (pretrained/stage_3/models/td3_best.pt, extracted weights-only into

@@ -95,6 +95,22 @@ def test_replay_ring_wraps():
     assert int(i.min()) == 0 and int(i.max()) == 9  # (rand * size).astype(int) over the filled slots
 
 
+def test_uniform_sampling_reaches_every_slot_past_2_24():
+    """Fill levels past 2^24 (a C5 round stores 65 536 x 500 = 32.8 M transitions): float64 uniforms and an
+    exact integer fill level keep every slot reachable (float32 would draw only even slots there) and never
+    index past the filled range."""
+    ring = ReplayRing(4, device="cpu")
+    size = 2 ** 25 + 3
+    ring.size_t.fill_(size)  # sampling reads only the fill level
+    torch.manual_seed(0)
+    i = ring.sample_indices(1_000_000)
+    assert int(i.min()) >= 0 and int(i.max()) <= size - 1
+    odd = float((i % 2 == 1).double().mean())
+    assert abs(odd - 0.5) < 0.005, odd
+    hi = float((i >= size // 2).double().mean())
+    assert abs(hi - 0.5) < 0.005, hi
+
+
 class _RefPER:
     """rl/replay/prioritized_buffer.py:6-69 weight bookkeeping, restated with numpy (one push at a time)."""
 
