@@ -11,11 +11,21 @@
   one ``hk_step`` launch per time step.
 
 Differences from running the reference protocol serially (documented, statistical only): the opponent's
-phase increments come from the per-arena Philox stream instead of the process-global ``np.random``, and
-every episode starts from a fresh BasicOpponent phase.  One reference env object reused across the 100
-episodes toggles ``one_starts`` on every reset; episode i therefore starts with ``one_starts = (i % 2 ==
-1)`` here as there.
+phase increments come from the per-arena Philox stream instead of the process-global ``np.random``.  The
+reference's Evaluator reuses one env -- and so one BasicOpponent -- for all its episodes and evaluations
+(rl/main.py:37-51), so an episode starts wherever the opponent's phase walk (U(0, 0.2) per step) has got to:
+``opponent_phase="walked"`` (default) starts every episode at a phase uniform on [0, 2 pi), "fresh" at a new
+BasicOpponent's U(0, pi).  One reference env object reused across the 100 episodes toggles ``one_starts`` on
+every reset; episode i therefore starts with ``one_starts = (i % 2 == 1)`` here as there (100 is even, so every
+evaluation of a run starts alike).
+
+``replicas`` = R plays each of the ``episodes`` placements R times (R x episodes arenas, placement i of every
+replica from ``reset(seed=seed + i)``), each replica with its own opponent phases: the per-placement win
+frequencies estimate the conditional win probability of each of the reference's fixed evaluation placements
+(tests/test_gpu_checkpoints.py).
 """
+import math
+
 import numpy as np
 import torch
 
@@ -69,26 +79,35 @@ def reset_params(episodes, seed, mode=Mode.NORMAL, first_reset=0):
 
 @torch.no_grad()
 def evaluate(policy, episodes=100, seed=42, weak_opponent=False, mode=Mode.NORMAL, device="cuda:0",
-             player1=None):
+             player1=None, replicas=1, opponent_phase="walked", phase_seed=None, per_episode=False):
     """Win rate and mean return of ``policy`` (obs [N,18] tensor -> actions [N,4]) against BasicOpponent.
 
     ``player1`` = "strong" / "weak" evaluates the fused BasicOpponent as player 1 instead of ``policy``
-    (the reference notebook's BasicOpponent-vs-BasicOpponent study).  Returns a dict with win / draw /
-    loss rates, mean return and mean episode length."""
+    (the reference notebook's BasicOpponent-vs-BasicOpponent study).  ``replicas``, ``opponent_phase``: see the
+    module docstring; ``phase_seed`` seeds the walked phases (default ``seed``).  Returns a dict with win / draw /
+    loss rates, mean return and mean episode length over all replicas x episodes games; ``per_episode`` adds
+    ``winner`` [replicas, episodes] (+1 / 0 / -1)."""
     from .vec_env import VecHockeyEnv
 
+    if opponent_phase not in ("walked", "fresh"):
+        raise ValueError("opponent_phase must be 'walked' or 'fresh'")
+    reps = int(replicas)
+    n = episodes * reps
     p1 = player1 if player1 is not None else "external"
-    env = VecHockeyEnv(episodes, keep_mode=True, mode=mode, device=device,
+    env = VecHockeyEnv(n, keep_mode=True, mode=mode, device=device,
                        policies=(p1, "weak" if weak_opponent else "strong"), auto_reset=False, seed=seed)
     params, max_t, _ = reset_params(episodes, seed, mode)
-    env.reset_params(params)
+    env.reset_params(np.tile(params, (reps, 1)))
+    if opponent_phase == "walked":
+        rng = np.random.default_rng(seed if phase_seed is None else phase_seed)
+        env.opponent_phase(rng.uniform(0, 2 * np.pi, (n, 2)))
     obs, _ = env.observe()
     dev = env.device
-    ret = torch.zeros(episodes, dtype=torch.float64, device=dev)
-    length = torch.zeros(episodes, dtype=torch.int64, device=dev)
-    winner = torch.zeros(episodes, dtype=torch.float32, device=dev)
-    live = torch.ones(episodes, dtype=torch.bool, device=dev)
-    act = torch.zeros((episodes, 8), dtype=torch.float32, device=dev)
+    ret = torch.zeros(n, dtype=torch.float64, device=dev)
+    length = torch.zeros(n, dtype=torch.int64, device=dev)
+    winner = torch.zeros(n, dtype=torch.float32, device=dev)
+    live = torch.ones(n, dtype=torch.bool, device=dev)
+    act = torch.zeros((n, 8), dtype=torch.float32, device=dev)
     for _ in range(max_t + 1):  # the longest episode is max_t + 1 steps (done when time >= max_t)
         if player1 is None:
             act[:, :4] = policy(obs).float()
@@ -103,9 +122,12 @@ def evaluate(policy, episodes=100, seed=42, weak_opponent=False, mode=Mode.NORMA
             break
     env.close()
     w = winner.cpu().numpy()
-    return {"episodes": episodes, "win": float((w == 1).mean()), "draw": float((w == 0).mean()),
-            "loss": float((w == -1).mean()), "mean_return": float(ret.mean().item()),
-            "mean_length": float(length.double().mean().item())}
+    out = {"episodes": n, "win": float((w == 1).mean()), "draw": float((w == 0).mean()),
+           "loss": float((w == -1).mean()), "mean_return": float(ret.mean().item()),
+           "mean_length": float(length.double().mean().item())}
+    if per_episode:
+        out["winner"] = w.reshape(reps, episodes).astype(np.int8)
+    return out
 
 
 # Hockey-Env.ipynb:940-2154 (cells 51-57): 1000 strong-vs-strong BasicOpponent games, unseeded resets on one
@@ -183,3 +205,61 @@ def study_zscores(per_game, ref=NOTEBOOK_STUDY):
     var1 = (resid ** 2).mean(0) / L.mean() ** 2
     out["obs_mean"] = [z(mu[k], ref["obs_mean"][k], var1[k]) for k in range(18)]
     return out
+
+
+def recorded_rate_z(winner, recorded):
+    """z-score of a win rate the reference recorded over its fixed evaluation placements against this simulator.
+
+    ``winner`` [R, E]: R replicas of the reference's E evaluation placements (``evaluate(..., replicas=R,
+    per_episode=True)``).  Given the placements, the reference's only randomness is its opponent's phase, so the
+    recorded rate is a mean of E Bernoulli(p_i), p_i = the win probability from placement i, which the replicas
+    estimate (shrunk to (k_i + 1/2) / (R + 1) so that no variance is zero).  Under the hypothesis that the
+    simulator is the reference's, recorded - mean(p_i) has variance sum p_i (1 - p_i) / E^2 (the recorded rate)
+    + the same / R (this estimate).  Returns a dict with z = (recorded - estimate) / se and, for comparison, the
+    binomial z that ignores the fixed placements."""
+    w = np.asarray(winner)
+    reps, e = w.shape
+    k = (w == 1).sum(0).astype(np.float64)
+    p_i = k / reps
+    q_i = (k + 0.5) / (reps + 1.0)
+    est = float(p_i.mean())
+    var1 = float((q_i * (1 - q_i)).sum()) / e ** 2
+    se = math.sqrt(var1 * (1.0 + 1.0 / reps))
+    pb = min(max(est, 0.5 / (reps * e)), 1 - 0.5 / (reps * e))
+    se_b = math.sqrt(pb * (1 - pb) / e + pb * (1 - pb) / (reps * e))
+    return {"recorded": float(recorded), "estimate": est, "se": se, "z": (float(recorded) - est) / se,
+            "z_binomial": (float(recorded) - est) / se_b, "replicas": reps, "placements": e}
+
+
+def checkpoint_pins(fixture, replicas=64, device="cuda:0"):
+    """Every shipped checkpoint against its recorded evaluation (tests/golden/checkpoint_actors.npz, written by
+    tests/golden/extract_checkpoint_actors.py): each actor runs the reference's evaluation protocol on R =
+    ``replicas`` replicas of the reference's own 100 placements (reset seeds run_seed + i) against the strong and,
+    where the run evaluated it, the weak bot.  Returns one row per recorded rate with its z (recorded_rate_z), and
+    whether the rate took part in the run's best-checkpoint selection: a td3_best.pt is the evaluation whose score
+    beat the running best (rl/utils/model_manager.py:15-23), so the rates behind that score are maxima of a noisy
+    series and sit above the policy's own rate by construction."""
+    import json
+
+    z = np.load(fixture) if isinstance(fixture, (str, bytes)) or hasattr(fixture, "__fspath__") else fixture
+    meta = json.loads(str(z["meta"]))
+    rows = []
+    for k, ck in enumerate(meta["checkpoints"]):
+        actor = Actor().to(device)
+        with torch.no_grad():
+            for name, p in actor.named_parameters():
+                p.copy_(torch.from_numpy(z[f"{k}/{name.replace('.', '_')}"]))
+        actor.eval()
+        for opp, rec in (("strong", ck["wr_strong"]), ("weak", ck["wr_weak"])):
+            if rec is None:
+                continue
+            r = evaluate(actor, episodes=ck["eval_episodes"], seed=ck["eval_seed"], weak_opponent=opp == "weak",
+                         device=device, replicas=replicas, phase_seed=1000 + 2 * k + (opp == "weak"),
+                         per_episode=True)
+            row = recorded_rate_z(r["winner"], rec)
+            score = ck["score"]
+            selected = ck["kind"] == "best" and (score in ("min", "winrates") or score == opp)
+            row.update(checkpoint=ck["name"], kind=ck["kind"], opponent=opp, eval_index=ck["eval_index"],
+                       n_evals=ck["n_evals"], selected=selected, mean_length=r["mean_length"])
+            rows.append(row)
+    return rows

@@ -65,3 +65,36 @@ def test_checkpoint_policy_evaluation_runs(tmp_path):
     r = evaluate(actor, episodes=256, seed=42, weak_opponent=True)
     assert abs(r["win"] + r["draw"] + r["loss"] - 1.0) < 1e-9
     assert 1.0 <= r["mean_length"] <= 251.0 and np.isfinite(r["mean_return"])
+
+
+def test_checkpoint_fixture_matches_stage3_extraction():
+    """tests/golden/checkpoint_actors.npz holds the 12 distinct shipped actors with their recorded evaluations;
+    its stage-3 best actor is the one tests/golden/stage3_actor.npz extracted (same eval index, same weights)."""
+    import json
+    import os
+
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(g, "checkpoint_actors.npz"))
+    meta = json.loads(str(z["meta"]))
+    cks = meta["checkpoints"]
+    assert len(cks) == 12 and len(meta["skipped"]) == 1
+    assert sum(c["wr_weak"] is not None for c in cks) + len(cks) == 20
+    s3 = np.load(os.path.join(g, "stage3_actor.npz"))
+    k = [i for i, c in enumerate(cks) if c["name"] == "pretrained/stage_3:best"][0]
+    assert cks[k]["eval_index"] == int(s3["best_eval_index"]) and cks[k]["wr_strong"] == float(s3["wr_strong"])
+    for name in ("fc1_weight", "fc1_bias", "fc2_weight", "fc2_bias", "fc3_weight", "fc3_bias"):
+        assert np.array_equal(z[f"{k}/{name}"], s3[name])
+    for c in cks:  # td3_last is the last evaluation of its run; td3_best one of them
+        assert 0 <= c["eval_index"] < c["n_evals"] and (c["kind"] == "best" or c["eval_index"] == c["n_evals"] - 1)
+
+
+def test_recorded_rate_z_statistic():
+    from hockey_amd.evaluate import recorded_rate_z
+
+    rng = np.random.default_rng(0)
+    p = rng.uniform(0.3, 1.0, 100)
+    w = (rng.uniform(size=(64, 100)) < p).astype(np.int8)
+    r = recorded_rate_z(w, p.mean())
+    assert abs(r["estimate"] - p.mean()) < 0.02 and abs(r["z"]) < 3
+    # the conditional se is below the binomial one (placements fixed)
+    assert abs(r["z"]) >= abs(r["z_binomial"]) - 1e-12
