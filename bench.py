@@ -213,13 +213,13 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
 
     q = hw_queues()
     S, n = min(args.streams, q - 1), args.arenas
-    if S < 2 or n % S:
+    if S < 2 or n < S:
         return None
-    m = n // S
+    sizes = [n // S + (k < n % S) for k in range(S)]  # contiguous shards, sizes differing by at most one
     envs, ios, streams = [], [], []
     for k in range(S):
-        e = VecHockeyEnv(m, device=dev, policies=pol, auto_reset=True, seed=args.seed,
-                         arena_offset=shard_offset(rank, n) + k * m)
+        e = VecHockeyEnv(sizes[k], device=dev, policies=pol, auto_reset=True, seed=args.seed,
+                         arena_offset=shard_offset(rank, n) + sum(sizes[:k]))
         e.reset()
         preroll(e, args.preroll, N)
         io = N.StepIO()
@@ -253,7 +253,7 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
         elapsed = float(t.item())
     for e in envs:
         e.close()
-    return {"streams": S, "arenas_per_stream": m, "hw_queues": q, "value": n * world * args.steps / elapsed,
+    return {"streams": S, "arenas_per_stream": sizes, "hw_queues": q, "value": n * world * args.steps / elapsed,
             "unit": "env-steps/s", "ms_per_step": elapsed / args.steps * 1e3}
 
 
