@@ -55,6 +55,25 @@ def main():
            "updates_per_round": updates_for(cfg, n, cfg.max_steps), "eval_episodes": args.eval_episodes,
            "reference_wr_weak": REF_WR_WEAK, "evals": []}
     t_start = time.time()
+    hist = {"rounds": 0}  # per-round stats of train() since the last evaluation (diagnostics)
+
+    def log(rnd, st):
+        hist["st"] = st
+
+    last = {"env_steps": 0, "rounds": 0, "critic": 0, "actor": 0}
+
+    def diag():
+        st = hist.get("st")
+        if st is None:
+            return {}
+        r0, c0, a0 = last["rounds"], last["critic"], last["actor"]
+        nr = len(st["mean_reward"])
+        cl, al = st["critic_loss"][c0:], st["actor_loss"][a0:]
+        d = {"mean_return": sum(st["mean_reward"][r0:]) / max(1, nr - r0),
+             "env_steps_per_episode": (st["env_steps"] - last["env_steps"]) / max(1, (nr - r0) * n),
+             "critic_loss": sum(cl) / max(1, len(cl)), "actor_loss": sum(al) / max(1, len(al))}
+        last.update(env_steps=st["env_steps"], rounds=nr, critic=len(st["critic_loss"]), actor=len(st["actor_loss"]))
+        return d
 
     def eval_fn(agent, episodes):
         agent.actor.eval()
@@ -62,7 +81,8 @@ def main():
         s = evaluate(agent.actor, episodes=args.eval_episodes, seed=agent.seed, weak_opponent=False, device=dev)
         agent.actor.train()
         rec = {"episode": episodes, "updates": agent.train_step, "wr_weak": w["win"], "wr_strong": s["win"],
-               "r_weak": w["mean_return"], "r_strong": s["mean_return"], "wall_s": time.time() - t_start}
+               "r_weak": w["mean_return"], "r_strong": s["mean_return"], "draw_weak": w["draw"],
+               "len_weak": w["mean_length"], "wall_s": time.time() - t_start, "train": diag()}
         out["evals"].append(rec)
         with open(args.out, "w") as f:
             json.dump(out, f, indent=1)
@@ -70,7 +90,7 @@ def main():
         return rec
 
     agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, device=dev, seed=args.seed, eval_fn=eval_fn,
-                      graphs=not args.no_graphs, episode_end=args.episode_end)
+                      graphs=not args.no_graphs, episode_end=args.episode_end, log=log)
     torch.cuda.synchronize()
     wr = [e["wr_weak"] for e in out["evals"]]
     first = next((e for e in out["evals"] if e["wr_weak"] >= 0.9), None)
