@@ -284,8 +284,10 @@ class TD3:
         c = self.cfg
         with torch.no_grad():
             ta = self.target_actor(s2)
-            noise = torch.clamp(torch.randn_like(ta) * c.target_action_noise_scale, -c.target_action_noise_clip,
-                                c.target_action_noise_clip)
+            raw = getattr(self, "_noise_override", None)  # tests: the reference's own N(0, scale) draw
+            if raw is None:
+                raw = torch.randn_like(ta) * c.target_action_noise_scale
+            noise = torch.clamp(raw, -c.target_action_noise_clip, c.target_action_noise_clip)
             ta = torch.clamp(ta + noise, -1.0, 1.0)
             q1, q2 = self.target_critic(s2, ta)
             return r + c.gamma * (1 - d) * torch.minimum(q1, q2)
@@ -370,9 +372,22 @@ class TD3:
         self.noise.reset()
 
     def checkpoint(self):
-        """The reference's td3_*.pt layout (policy / critic / target_policy / target_critic)."""
-        return {"policy": self.actor.state_dict(), "critic": self.critic.state_dict(),
-                "target_policy": self.target_actor.state_dict(), "target_critic": self.target_critic.state_dict()}
+        """The reference's td3_*.pt layout (policy / critic / target_policy / target_critic); tensors are copies (the
+        fused learner keeps the parameters as views of one flat buffer per network)."""
+        def sd(m):
+            return {k: v.detach().clone() for k, v in m.state_dict().items()}
+        return {"policy": sd(self.actor), "critic": sd(self.critic), "target_policy": sd(self.target_actor),
+                "target_critic": sd(self.target_critic)}
+
+
+FUSED_MIN_BATCH = 4096  # fused="auto": the MFMA learner from this batch up (C5 draws 16 384 per update)
+
+
+def fused_available():
+    """True when the fused learner library is built (hockey_amd/_lib/libhockey_learner.so)."""
+    from .learner_hip import LIB_PATH
+    import os
+    return os.path.exists(LIB_PATH)
 
 
 class Learner:
@@ -380,16 +395,35 @@ class Learner:
 
     With ``graphs`` on a GPU the pair (critic update; critic + delayed actor + Polyak) is captured once as a HIP
     graph after ``warm_pairs`` eager pairs and replayed: the same updates, launched as one graph instead of a few
-    hundred kernel launches.  Losses accumulate on the device (no host sync per update)."""
+    hundred kernel launches.  Losses accumulate on the device (no host sync per update).
 
-    def __init__(self, agent, ring, batch, graphs=True, warm_pairs=3):
+    fused: True runs every update through the fused fp32 MFMA kernels (hockey_amd.learner_hip: a handful of HIP
+    kernels per update; batches that are multiples of 256, GPU only, fails loudly without the library); False
+    through PyTorch ops; "auto" (default) picks fused for GPU batches of at least FUSED_MIN_BATCH when the library is
+    built."""
+
+    def __init__(self, agent, ring, batch, graphs=True, warm_pairs=3, fused="auto"):
         self.agent, self.ring, self.batch = agent, ring, int(batch)
         self.use_graph = bool(graphs) and agent.device.type == "cuda" and agent.cfg.policy_update_freq == 2
         self.warm_left = int(warm_pairs)
         self.graph = None
         self.acc = torch.zeros(4, dtype=torch.float64, device=agent.device)  # sum critic, sum actor, n c, n a
+        if fused == "auto":
+            fused = (agent.device.type == "cuda" and self.batch >= FUSED_MIN_BATCH and self.batch % 256 == 0 and
+                     fused_available())
+        self.fused = None
+        if fused:
+            from .learner_hip import FusedLearner
+            self.fused = FusedLearner(agent, ring, self.batch)
+            self.fused.set_loss_accumulator(self.acc)
 
     def _one(self, train_actor=None):
+        if self.fused is not None:
+            if train_actor is None:
+                self.agent.train_step += 1
+                train_actor = self.agent.train_step % self.agent.cfg.policy_update_freq == 0
+            self.fused.update(train_actor)
+            return
         s, a, r, s2, d, iw = self.ring.sample(self.batch)
         al, cl = self.agent._update_tensors(s, a, r, s2, d, iw, self.ring, train_actor)
         self.acc[0] += cl
@@ -441,7 +475,7 @@ class Learner:
 def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_per_round=None, mode=Mode.NORMAL,
           curriculum=None, use_self_play=None, self_play_interval=None, pool_size=None, reset="seeded", log=None,
           replay_capacity=None, graphs=True, eval_fn=None, learner_batch=None, timing=False, replay_ratio=None,
-          env=None, on_step=None, episode_end="max_steps"):
+          env=None, on_step=None, episode_end="max_steps", fused="auto"):
     """Batched TD3 training (rl/training/train.py TD3Trainer.train).  Each round runs ``max_steps`` steps of
     ``n_arenas`` parallel episodes (no break on done), stores every transition, then performs the learner
     updates of those episodes at the replay ratio: ``ratio * n_arenas * max_steps / B`` updates of batch B =
@@ -456,7 +490,7 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     arenas); "device" uses the kernel's Philox placement (same distribution, no host work).
     eval_fn(agent, episodes_done) is called every ``cfg.eval_interval`` episodes.  timing: synchronise around each
     round's collection and updates and record their wall seconds in ``stats["round_time"]``.  Returns
-    (agent, stats).  env: a VecHockeyEnv-shaped batch of n_arenas arenas to train on (default: a new
+    (agent, stats).  fused: the learner path (Learner).  env: a VecHockeyEnv-shaped batch of n_arenas arenas to train on (default: a new
     VecHockeyEnv on ``device``; the CPU tests pass the kernel source's host build).  on_step(obs, action,
     reward, next_obs, done, step_result) sees every stored transition (test hook).
 
@@ -487,7 +521,7 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     ring = (PrioritizedRing(cap, device=device, beta=cfg.beta) if cfg.prioritized_replay
             else ReplayRing(cap, device=device))
     batch = int(learner_batch or cfg.batch_size)
-    learner = Learner(agent, ring, batch, graphs=graphs)
+    learner = Learner(agent, ring, batch, graphs=graphs, fused=fused)
     updates = updates_per_round if updates_per_round is not None else \
         updates_for(cfg, n_arenas, cfg.max_steps, batch, replay_ratio)
     act8 = torch.zeros((n_arenas, 8), device=device)

@@ -1,6 +1,8 @@
 """Where a C5 learner update's time goes: hockey_amd.td3.Learner on a ring of random transitions, batch B (default
-16 384, the C5 learner batch), K updates after a warm-up.  Prints ms per update; run under
-`rocprofv3 --kernel-trace --stats` for the per-kernel split.  Usage: python scripts/learner_profile.py [B] [K]"""
+16 384, the C5 learner batch), K updates after a warm-up, for the PyTorch path and the fused MFMA path (each eager
+and graph-replayed).  Prints ms per update and the fused path's achieved fp32 FLOP/s (algorithmic FLOPs of
+hockey_amd.learner_hip.update_flops); run under `rocprofv3 --kernel-trace --stats` for the per-kernel split.
+Usage: python scripts/learner_profile.py [B] [K] [paths: torch,fused]"""
 import json
 import os
 import sys
@@ -24,13 +26,20 @@ n = 1 << 20
 ring.push(torch.randn(n, 18, device=dev, generator=g), torch.rand(n, 4, device=dev, generator=g) * 2 - 1,
           torch.randn(n, device=dev, generator=g), torch.randn(n, 18, device=dev, generator=g),
           (torch.rand(n, device=dev, generator=g) < 0.01).float())
+paths = (sys.argv[3] if len(sys.argv) > 3 else "torch,fused").split(",")
 out = {"batch": B, "updates": K, "blas": str(torch.backends.cuda.preferred_blas_library())}
-for graphs in (False, True):
-    L = Learner(agent, ring, B, graphs=graphs)
-    L.run(20)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    L.run(K)
-    torch.cuda.synchronize()
-    out["ms_per_update_graphs" if graphs else "ms_per_update_eager"] = (time.perf_counter() - t0) / K * 1e3
-print(json.dumps(out))
+for path in paths:
+    for graphs in (False, True):
+        agent = TD3(TD3Config(), dev, seed=0)
+        L = Learner(agent, ring, B, graphs=graphs, fused=(path == "fused"))
+        L.run(20)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        L.run(K)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / K * 1e3
+        out[f"{path}_ms_per_update_{'graphs' if graphs else 'eager'}"] = ms
+        if path == "fused":
+            from hockey_amd.learner_hip import update_flops
+            out[f"fused_tflops_{'graphs' if graphs else 'eager'}"] = update_flops(B) / (ms * 1e-3) / 1e12
+        print(json.dumps(out), flush=True)

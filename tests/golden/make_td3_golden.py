@@ -8,7 +8,12 @@ Protocol: hidden size 32; initial weights = hockey_amd.td3.TD3(seed=0, h=32)'s; 
 torch.manual_seed(2000 + k) set just before it (the target-smoothing noise).  Recorded: every update's critic
 and actor loss, and the final actor / critic / target parameters (state_dict order).
 
-Usage: python tests/golden/make_td3_golden.py"""
+G9b (``--wide``): the same protocol at the C5 network and batch shapes the fused HIP learner runs -- hidden size 256,
+batch 256, 10 updates -- into g9b_td3_learner_h256.npz; the target noise of update k is what the reference draws
+(torch.normal(0, 0.2, (B, 4)) under torch.manual_seed(2000 + k) on the CPU), recorded so the GPU path can be fed the
+same numbers.
+
+Usage: python tests/golden/make_td3_golden.py [--wide]"""
 import copy
 import os
 import sys
@@ -36,17 +41,19 @@ def batch(k):
     return s, a, r, s2, d
 
 
-def main():
+def main(h=H, b=B, k_updates=K, out_name="g9_td3_learner.npz"):
     # the reference is imported here only: tests import this module for batch() without /root/reference
+    global B
+    B = b
     from rl.td3.config import TD3Config as RefConfig
     from rl.td3.learner import TD3Learner
     from rl.td3.networks import ActorNetwork, TwinQNetwork
 
-    init = TD3(TD3Config(), device="cpu", seed=0, h=H)
+    init = TD3(TD3Config(), device="cpu", seed=0, h=h)
     cfg = RefConfig()
-    pol = ActorNetwork(18, 4, h=H)
+    pol = ActorNetwork(18, 4, h=h)
     pol.load_state_dict(init.actor.state_dict())
-    crit = TwinQNetwork(18, 4, H, action_low=-torch.ones(4), action_high=torch.ones(4))
+    crit = TwinQNetwork(18, 4, h, action_low=-torch.ones(4), action_high=torch.ones(4))
     crit.load_state_dict(init.critic.state_dict())
     tpol, tcrit = copy.deepcopy(pol), copy.deepcopy(crit)
     for net in (tpol, tcrit):
@@ -59,19 +66,26 @@ def main():
         pass
 
     ref = TD3Learner(pol, crit, tpol, tcrit, copt, aopt, _NoBuffer(), None, cfg, "cpu", cfg.beta)
-    closs, aloss = [], []
-    for k in range(K):
+    closs, aloss, noise = [], [], []
+    for k in range(k_updates):
+        torch.manual_seed(2000 + k)
+        noise.append(torch.normal(0, cfg.target_action_noise_scale, size=(B, 4)).numpy())  # what compute_target draws
         torch.manual_seed(2000 + k)
         al, cl = ref.update(*batch(k))
         closs.append(cl)
         aloss.append(np.nan if al is None else al)
     out = {"critic_loss": np.array(closs, np.float64), "actor_loss": np.array(aloss, np.float64)}
+    if out_name != "g9_td3_learner.npz":
+        out.update(noise=np.stack(noise), h=np.array(h), b=np.array(b))
     for name, net in (("actor", pol), ("critic", crit), ("target_actor", tpol), ("target_critic", tcrit)):
         for key, v in net.state_dict().items():
             out[f"{name}/{key}"] = v.numpy()
-    np.savez(os.path.join(OUT, "g9_td3_learner.npz"), **out)
-    print("wrote g9_td3_learner.npz", len(out), "arrays")
+    np.savez_compressed(os.path.join(OUT, out_name), **out)
+    print("wrote", out_name, len(out), "arrays")
 
 
 if __name__ == "__main__":
-    main()
+    if "--wide" in sys.argv:
+        main(h=256, b=256, k_updates=10, out_name="g9b_td3_learner_h256.npz")
+    else:
+        main()

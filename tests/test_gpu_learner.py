@@ -1,0 +1,161 @@
+"""The GPU learner paths of hockey_amd.td3 (BASELINE C5) against the reference's own TD3Learner.
+
+* G9 (hidden 32, batch 64; tests/golden/make_td3_golden.py) through the eager PyTorch learner on the GPU;
+* G9b (hidden 256, batch 256, 10 updates: the C5 network shapes) through the fused fp32 MFMA learner
+  (hockey_amd.learner_hip, csrc/hk_learner.hip) fed the reference's own batches and target noise;
+* the fused learner against the eager learner on the same ring, slots and noise at a C5-like batch.
+
+Tolerances: fp32 with a different summation order (MFMA fma chains vs the reference's BLAS): losses within
+1e-4 relative, parameters within 1e-5 absolute after the sequence (Adam steps are ~lr = 4e-4 per update, so a
+wrong gradient sign or scale moves a parameter by ~1e-4 per update and fails)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from hockey_amd.td3 import TD3, Learner, ReplayRing, TD3Config  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEV = "cuda:0"
+LOSS_RTOL, PARAM_ATOL = 1e-4, 1e-5
+
+
+def _golden_batches():
+    sys.path.insert(0, GOLDEN)
+    import make_td3_golden as M
+    return M
+
+
+def _close_params(agent, g, atol):
+    bad = []
+    for name, net in (("actor", agent.actor), ("critic", agent.critic), ("target_actor", agent.target_actor),
+                      ("target_critic", agent.target_critic)):
+        for key, v in net.state_dict().items():
+            d = float(np.abs(v.detach().cpu().numpy() - g[f"{name}/{key}"]).max())
+            if d > atol:
+                bad.append((f"{name}/{key}", d))
+    return bad
+
+
+def test_eager_learner_on_gpu_matches_reference_learner_g9():
+    M = _golden_batches()
+    g9 = np.load(os.path.join(GOLDEN, "g9_td3_learner.npz"))
+    agent = TD3(TD3Config(), device="cpu", seed=0, h=M.H)
+    gpu = TD3(TD3Config(), device=DEV, seed=0, h=M.H)
+    for src, dst in ((agent.actor, gpu.actor), (agent.critic, gpu.critic), (agent.target_actor, gpu.target_actor),
+                     (agent.target_critic, gpu.target_critic)):
+        dst.load_state_dict(src.state_dict())
+    B = 64
+    for k in range(M.K):
+        s, a, r, s2, d = (t.to(DEV) for t in M.batch(k))
+        torch.manual_seed(2000 + k)
+        noise = torch.normal(0, 0.2, size=(B, 4))  # the reference's CPU draw, fed to the GPU update
+        gpu._noise_override = noise.to(DEV)
+        al, cl = gpu.update(s, a, r, s2, d)
+        assert abs(float(cl) - g9["critic_loss"][k]) <= LOSS_RTOL * max(1.0, abs(g9["critic_loss"][k])), k
+        if al is not None:
+            assert abs(float(al) - g9["actor_loss"][k]) <= LOSS_RTOL * max(1.0, abs(g9["actor_loss"][k])), k
+    assert not _close_params(gpu, g9, PARAM_ATOL)
+
+
+def _ring_with(batches, device):
+    """A ring holding the concatenated golden batches in order (slot = k * B + i)."""
+    n = sum(b[0].shape[0] for b in batches)
+    ring = ReplayRing(n, device=device)
+    for s, a, r, s2, d in batches:
+        ring.push(s.to(device), a.to(device), r.to(device), s2.to(device), d.to(device))
+    return ring
+
+
+def test_fused_learner_matches_reference_learner_g9b():
+    """G9b: the reference's TD3Learner at hidden 256 / batch 256 over 10 updates (5 actor updates, 5 Polyak
+    averagings) vs the fused MFMA learner fed the same batches (ring slots k*256 .. k*256+255) and the same
+    target noise."""
+    from hockey_amd.learner_hip import FusedLearner
+
+    M = _golden_batches()
+    g = np.load(os.path.join(GOLDEN, "g9b_td3_learner_h256.npz"))
+    B, K = int(g["b"]), len(g["critic_loss"])
+    M.B = B
+    batches = [M.batch(k) for k in range(K)]
+    agent = TD3(TD3Config(), device=DEV, seed=0, h=256)
+    init = TD3(TD3Config(), device="cpu", seed=0, h=256)  # the golden's initial weights (CPU init of seed 0)
+    for src, dst in ((init.actor, agent.actor), (init.critic, agent.critic), (init.target_actor, agent.target_actor),
+                     (init.target_critic, agent.target_critic)):
+        dst.load_state_dict(src.state_dict())
+    ring = _ring_with(batches, DEV)
+    fl = FusedLearner(agent, ring, B)
+    acc = torch.zeros(4, dtype=torch.float64, device=DEV)
+    fl.set_loss_accumulator(acc)
+    for k in range(K):
+        idx = torch.arange(k * B, (k + 1) * B, device=DEV)
+        train_actor = (k + 1) % 2 == 0
+        before = acc.clone()
+        fl.update(train_actor, idx=idx, noise=torch.from_numpy(g["noise"][k]).to(DEV))
+        d = (acc - before).cpu().numpy()
+        assert abs(d[0] - g["critic_loss"][k]) <= LOSS_RTOL * max(1.0, abs(g["critic_loss"][k])), (k, d[0])
+        if train_actor:
+            assert abs(d[1] - g["actor_loss"][k]) <= LOSS_RTOL * max(1.0, abs(g["actor_loss"][k])), (k, d[1])
+    torch.cuda.synchronize()
+    bad = _close_params(agent, g, PARAM_ATOL)
+    assert not bad, bad[:8]
+
+
+def test_fused_learner_matches_eager_learner_on_ring():
+    """Fused vs eager (PyTorch) learner from the same weights and ring, with the same torch RNG stream (slots, then
+    target noise): 8 updates of 4096 samples."""
+    cfg = TD3Config()
+    torch.manual_seed(7)
+    cap = 50_000
+    ring_e = ReplayRing(cap, device=DEV)
+    s, s2 = torch.randn(cap, 18, device=DEV), torch.randn(cap, 18, device=DEV)
+    a = torch.rand(cap, 4, device=DEV) * 2 - 1
+    r, d = torch.randn(cap, device=DEV), (torch.rand(cap, device=DEV) < 0.1).float()
+    ring_e.push(s, a, r, s2, d)
+    eager, fused = TD3(cfg, device=DEV, seed=3), TD3(cfg, device=DEV, seed=3)
+    le = Learner(eager, ring_e, 4096, graphs=False, fused=False)
+    lf = Learner(fused, ring_e, 4096, graphs=False, fused=True)
+    for k in range(8):
+        torch.manual_seed(100 + k)
+        le._one()
+        torch.manual_seed(100 + k)
+        lf._one()
+    ce, ae = le.take_losses()
+    cf, af = lf.take_losses()
+    assert abs(ce - cf) <= LOSS_RTOL * max(1.0, abs(ce)) and abs(ae - af) <= LOSS_RTOL * max(1.0, abs(ae)), (ce, cf, ae, af)
+    worst = 0.0
+    for ne, nf in ((eager.actor, fused.actor), (eager.critic, fused.critic), (eager.target_actor, fused.target_actor),
+                   (eager.target_critic, fused.target_critic)):
+        for (kk, ve), (_, vf) in zip(ne.state_dict().items(), nf.state_dict().items()):
+            worst = max(worst, float((ve - vf).abs().max()))
+    assert worst <= PARAM_ATOL, worst
+
+
+def test_fused_graph_replay_equals_fused_eager():
+    """The fused updates captured as a HIP graph (Learner's update pairs) give the same parameters as launching them
+    one by one: identical ring entries (sampling cannot matter) and no target noise make both paths deterministic,
+    and the kernels reduce in fixed orders (no atomics), so the parameters are bit-identical."""
+    nets = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        cfg = TD3Config(target_action_noise_scale=0.0)
+        agent = TD3(cfg, device=DEV, seed=0)
+        ring = ReplayRing(4096, device=DEV)
+        g = torch.Generator().manual_seed(1)
+        one = [torch.randn(1, 18, generator=g), torch.rand(1, 4, generator=g) * 2 - 1, torch.randn(1, generator=g),
+               torch.randn(1, 18, generator=g), torch.zeros(1)]
+        ring.push(*(t.expand(4096, *t.shape[1:]).contiguous().to(DEV) for t in one))
+        lr = Learner(agent, ring, 2048, graphs=graphs, warm_pairs=1, fused=True)
+        for _ in range(3):
+            lr.run(8)
+        assert agent.train_step == 24 and (lr.graph is not None) == graphs
+        torch.cuda.synchronize()
+        nets.append(torch.cat([p.detach().flatten() for p in list(agent.actor.parameters()) +
+                               list(agent.critic.parameters()) + list(agent.target_actor.parameters()) +
+                               list(agent.target_critic.parameters())]))
+    assert torch.equal(nets[0], nets[1]), (nets[0] - nets[1]).abs().max()

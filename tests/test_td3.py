@@ -393,3 +393,27 @@ def test_episode_end_done_stores_only_running_episodes():
         running -= int(d.sum())
     assert running == 0 and len(seen) <= 251
     assert stored < n * len(seen) or len(seen) == 251
+
+
+def test_learner_matches_reference_learner_g9b_wide():
+    """G9b (hidden 256, batch 256: the C5 network shapes; tests/golden/make_td3_golden.py --wide): the eager learner on
+    the CPU reproduces the reference's TD3Learner losses and parameters (float32 rounding only)."""
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    import make_td3_golden as M
+
+    g = np.load(os.path.join(GOLDEN, "g9b_td3_learner_h256.npz"))
+    M.B = int(g["b"])
+    agent = TD3(TD3Config(), device="cpu", seed=0, h=int(g["h"]))
+    for k in range(len(g["critic_loss"])):
+        torch.manual_seed(2000 + k)
+        al, cl = agent.update(*M.batch(k))
+        assert abs(float(cl) - g["critic_loss"][k]) <= 1e-5 * max(1.0, abs(g["critic_loss"][k])), k
+        if al is not None:
+            assert abs(float(al) - g["actor_loss"][k]) <= 1e-5 * max(1.0, abs(g["actor_loss"][k])), k
+    for name, net in (("actor", agent.actor), ("critic", agent.critic), ("target_actor", agent.target_actor),
+                      ("target_critic", agent.target_critic)):
+        for key, v in net.state_dict().items():
+            np.testing.assert_allclose(v.numpy(), g[f"{name}/{key}"], rtol=0, atol=1e-6, err_msg=f"{name}/{key}")
+    M.B = 64
