@@ -41,6 +41,17 @@ struct Tile {
   f4 v[16];
 };
 
+// tanh without branches: tanh|x| = (1 - t) / (1 + t), t = 2^(-2 log2(e) |x|) (v_exp_f32, v_rcp_f32), sign restored.
+// OCML's tanhf branches between a polynomial and an exp path per lane (exec-mask juggling around ~30 VALU per
+// call, a third of the critic kernel's instructions); this form is 7 VALU.  Its absolute error is a few 1e-8 near
+// 0 (the 1 - t cancellation) and below 2e-7 everywhere (checked against torch.tanh in
+// tests/test_gpu_learner.py), far inside the learner's stated fp32 tolerances.
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));
+  const float y = (1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t);
+  return copysignf(y, x);
+}
+
 // ------------------------------------------------------------------------------------------------ packed layouts
 // f1 [16 ob][64 lane][8]     : W1[16 ob + (l & 15)][4 s + (l >> 4)] for k-step s < 6 (0 past the input width)
 // fp [16 ob][16 kb][64 lane] : f4 over r of W2[16 ob + (l & 15)][16 kb + 4 (l >> 4) + r]        (forward)
@@ -81,20 +92,37 @@ __device__ __forceinline__ void gemm_in(const float *__restrict__ f1, const floa
   }
 }
 
-// out = P in, P a packed 256 x 256 operand (fp: W2 in; bp: W2^T in).  The A fragments of the next 16-neuron
-// k-block are loaded while the current one is multiplied.
-__device__ __forceinline__ void gemm256(const f4 *__restrict__ P, const Tile &in, Tile &out, int lane) {
+// out = P in, P a packed 256 x 256 operand (fp: W2 in; bp: W2^T in), a workgroup-collective call (all 4 waves).
+// The A fragments are the same for the workgroup's 4 waves: each 16-neuron k-block (16 KB) is loaded once per
+// workgroup into one of two LDS buffers (each thread 4 x 16 B) while the waves multiply the previous one, so the
+// L2 serves a quarter of the bytes.  bias != nullptr: `in` holds pre-activations and block kb is activated in
+// place (tanh(in + bias)) just before its first use, so the activation's VALU work overlaps the MFMAs of the
+// block before; on return `in` holds the activations.
+__device__ __forceinline__ void gemm256(const f4 *__restrict__ P, Tile &in, const float *__restrict__ bias, Tile &out,
+                                        int lane, f4 *sfrag) {
+  const int wave = threadIdx.x >> 6, q = lane >> 4;
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) out.v[ob] = z4();
-  f4 a[16];
+  f4 g[4];
 #pragma unroll
-  for (int ob = 0; ob < 16; ++ob) a[ob] = P[(ob * 16) * 64 + lane];
+  for (int i = 0; i < 4; ++i) g[i] = P[((4 * wave + i) * 16) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sfrag[(4 * wave + i) * 64 + lane] = g[i];
+  __syncthreads();
 #pragma unroll
   for (int kb = 0; kb < 16; ++kb) {
-    f4 an[16];
+    const f4 *buf = sfrag + (kb & 1) * 1024;
     if (kb + 1 < 16) {
 #pragma unroll
-      for (int ob = 0; ob < 16; ++ob) an[ob] = P[(ob * 16 + kb + 1) * 64 + lane];
+      for (int i = 0; i < 4; ++i) g[i] = P[((4 * wave + i) * 16 + kb + 1) * 64 + lane];
+    }
+    f4 a[16];
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) a[ob] = buf[ob * 64 + lane];
+    if (bias) {
+      const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * kb + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) in.v[kb][r] = tanh_fast(in.v[kb][r] + bb[r]);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -103,9 +131,11 @@ __device__ __forceinline__ void gemm256(const f4 *__restrict__ P, const Tile &in
       for (int ob = 0; ob < 16; ++ob) out.v[ob] = mfma(a[ob][r], b, out.v[ob]);
     }
     if (kb + 1 < 16) {
+      f4 *nb = sfrag + ((kb + 1) & 1) * 1024;
 #pragma unroll
-      for (int ob = 0; ob < 16; ++ob) a[ob] = an[ob];
+      for (int i = 0; i < 4; ++i) nb[(4 * wave + i) * 64 + lane] = g[i];
     }
+    __syncthreads();
   }
 }
 
@@ -115,17 +145,24 @@ __device__ __forceinline__ void bias_tanh(Tile &t, const float *__restrict__ b, 
   for (int ob = 0; ob < 16; ++ob) {
     const f4 bb = *reinterpret_cast<const f4 *>(b + 16 * ob + 4 * q);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) t.v[ob][r] = tanhf(t.v[ob][r] + bb[r]);
+    for (int r = 0; r < 4; ++r) t.v[ob][r] = tanh_fast(t.v[ob][r] + bb[r]);
   }
 }
 
-// the n_out (<= 4) outputs W3 h + b3 of this lane's sample, broadcast to every lane of the sample
-__device__ __forceinline__ f4 gemm_out(const f4 *__restrict__ fo, const Tile &h, const float *__restrict__ b3, int n_out,
-                                       int lane) {
+// the n_out (<= 4) outputs W3 h + b3 of this lane's sample, broadcast to every lane of the sample.  bias !=
+// nullptr: h holds pre-activations, activated in place (tanh(h + bias)) block by block as in gemm256.
+__device__ __forceinline__ f4 gemm_out(const f4 *__restrict__ fo, Tile &h, const float *__restrict__ bias,
+                                       const float *__restrict__ b3, int n_out, int lane) {
+  const int q = lane >> 4;
   f4 acc0 = z4(), acc1 = z4();
 #pragma unroll
   for (int kb = 0; kb < 16; ++kb) {
     const f4 a = fo[kb * 64 + lane];
+    if (bias) {
+      const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * kb + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h.v[kb][r] = tanh_fast(h.v[kb][r] + bb[r]);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (kb & 1) acc1 = mfma(a[r], h.v[kb][r], acc1);
@@ -158,12 +195,17 @@ __device__ __forceinline__ void tanh_back(Tile &t, const Tile &y) {
   for (int ob = 0; ob < 16; ++ob) t.v[ob] = t.v[ob] * (1.0f - y.v[ob] * y.v[ob]);
 }
 
-// sum over the 16 samples of a wave (lanes with equal lane >> 4)
+// sum over the 16 samples of a wave (lanes with equal lane >> 4: one DPP row), every lane of the row gets the sum:
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror -- four v_add with a DPP source
+template <int C>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), C, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
   return v;
 }
 
@@ -224,25 +266,24 @@ __device__ __forceinline__ void input_frags(const float *__restrict__ srow, cons
 
 // ------------------------------------------------------------------------------------------------ critic step
 // Q(x) of one critic network (forward only): its output for this lane's sample
-__device__ __forceinline__ float q_forward(const Net &c, const float (&x)[S1], Tile &h1, Tile &h2, int lane, int q) {
+__device__ __forceinline__ float q_forward(const Net &c, const float (&x)[S1], Tile &h1, Tile &h2, int lane,
+                                           f4 *sfrag) {
   gemm_in(c.f1(), x, h1, lane);
-  bias_tanh(h1, c.b1, q);
-  gemm256(c.fp(), h1, h2, lane);
-  bias_tanh(h2, c.b2, q);
-  return gemm_out(c.fo(), h2, c.b3, 1, lane)[0];
+  gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
+  return gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane)[0];
 }
 
 // one critic k of update_critic: forward on x, the weighted smooth-L1 (torch_utils.py:12-24; critic_loss =
-// (loss1 + loss2) * 0.5, each a batch mean) and the backward to the first layer
+// (loss1 + loss2) * 0.5, each a batch mean) and the backward to the first layer.  Stores H1, DZ1, DZ2 for the
+// weight gradients (their bias gradients are the column sums wgrad takes); dW3 / db3 as workgroup partials.
 __device__ __forceinline__ void critic_one(const hkl_critic_io &io, int k, const Net &c, const float (&x)[S1], float y,
-                                           float w, int64_t row, float *red, float &td, float &loss) {
+                                           float w, int64_t row, float *red, f4 *sfrag, float &td, float &loss) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4;
   Tile h1, h2;
   gemm_in(c.f1(), x, h1, lane);
-  bias_tanh(h1, c.b1, q);
-  gemm256(c.fp(), h1, h2, lane);
-  bias_tanh(h2, c.b2, q);
-  const float qv = gemm_out(c.fo(), h2, c.b3, 1, lane)[0];
+  gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
+  store_tile(io.h1[k], h1, row, q);
+  const float qv = gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane)[0];
   const float diff = qv - y, ad = fabsf(diff);
   loss += ad < 1.0f ? 0.5f * w * diff * diff : (ad - 0.5f) * w;
   const float g = (ad < 1.0f ? w * diff : (diff > 0.0f ? w : diff < 0.0f ? -w : 0.0f)) * (0.5f / (float)io.batch);
@@ -258,22 +299,19 @@ __device__ __forceinline__ void critic_one(const hkl_critic_io &io, int k, const
   back_out(c.w3, 1, f4{g, 0.0f, 0.0f, 0.0f}, t, q);
   tanh_back(t, h2);
   store_tile(io.dz2[k], t, row, q);
-  store_tile(io.h1[k], h1, row, q);
-  wg_neuron_sum(t, red, io.p_db2[k] + blockIdx.x * H, wave, lane);
   // dz1 = (W2^T dz2) * (1 - h1^2)
-  gemm256(c.bp(), t, h2, lane);
+  gemm256(c.bp(), t, nullptr, h2, lane, sfrag);
   tanh_back(h2, h1);
   store_tile(io.dz1[k], h2, row, q);
-  wg_neuron_sum(h2, red, io.p_db1[k] + blockIdx.x * H, wave, lane);
 }
 
 // compute_target + update_critic's forward / loss / backward for both critics (learner.py:75-136).
 __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
+  __shared__ f4 sfrag[2 * 16 * 64];
   __shared__ float red[4 * H];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, j = lane & 15;
-  const int64_t g = blockIdx.x;
-  const int64_t row = g * 64 + wave * 16 + j;  // this lane's sample (batch row)
-  const int64_t src = io.idx[row];             // its replay slot
+  const int64_t row = (int64_t)blockIdx.x * 64 + wave * 16 + j;  // this lane's sample (batch row)
+  const int64_t src = io.idx[row];                                // its replay slot
   const float *s_row = io.ring_s + src * 18, *s2_row = io.ring_s2 + src * 18;
   const float rwd = io.ring_r[src], dn = io.ring_d[src];
   const f4 act = *reinterpret_cast<const f4 *>(io.ring_a + src * 4);
@@ -287,18 +325,16 @@ __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
   input_frags(s2_row, z4(), false, x, q);
   Tile h1, h2;
   gemm_in(ta.f1(), x, h1, lane);
-  bias_tanh(h1, ta.b1, q);
-  gemm256(ta.fp(), h1, h2, lane);
-  bias_tanh(h2, ta.b2, q);
-  f4 a2 = gemm_out(ta.fo(), h2, ta.b3, 4, lane);
+  gemm256(ta.fp(), h1, ta.b1, h2, lane, sfrag);
+  const f4 a2 = gemm_out(ta.fo(), h2, ta.b2, ta.b3, 4, lane);
   f4 a2u;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const float t = fminf(fmaxf(tanhf(a2[c]) + nz[c], -1.0f), 1.0f);  // torch.clamp(target_action + noise, -1, 1)
+    const float t = fminf(fmaxf(tanh_fast(a2[c]) + nz[c], -1.0f), 1.0f);  // torch.clamp(target_action + noise, -1, 1)
     a2u[c] = unscale(t, io.act_low[c], io.act_range[c]);
   }
   input_frags(s2_row, a2u, true, x, q);
-  const float qt0 = q_forward(tq[0], x, h1, h2, lane, q), qt1 = q_forward(tq[1], x, h1, h2, lane, q);
+  const float qt0 = q_forward(tq[0], x, h1, h2, lane, sfrag), qt1 = q_forward(tq[1], x, h1, h2, lane, sfrag);
   const float y = rwd + io.gamma * (1.0f - dn) * fminf(qt0, qt1);
 
   // ---- critics on (s, a)
@@ -306,13 +342,17 @@ __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) au[c] = unscale(act[c], io.act_low[c], io.act_range[c]);
   input_frags(s_row, au, true, x, q);
-  if (q == 0) {  // X0 row (shared by both critics' dW1): 22 features, zero padded
+  {  // X0 row (shared by both critics' dW1): 22 features, zero padded; lane q writes 8 of its sample's 32
     float *xr = io.x0 + row * XP;
-    for (int f = 0; f < XP; ++f) xr[f] = f < 18 ? s_row[f] : f < 22 ? au[f - 18] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int f = 8 * q + e;
+      xr[f] = f < 18 ? s_row[f] : f < 22 ? au[f - 18] : 0.0f;
+    }
   }
   float td = 0.0f, loss = 0.0f;
-  critic_one(io, 0, cq[0], x, y, w, row, red, td, loss);
-  critic_one(io, 1, cq[1], x, y, w, row, red, td, loss);
+  critic_one(io, 0, cq[0], x, y, w, row, red, sfrag, td, loss);
+  critic_one(io, 1, cq[1], x, y, w, row, red, sfrag, td, loss);
   if (io.td && q == 0) io.td[row] = td * 0.5f;  // (|q1 - y| + |q2 - y|) / 2 (learner.py:163-170)
   const float ls = wg_scalar_sum(loss, red, wave, lane);
   if (threadIdx.x == 0) io.p_loss[blockIdx.x] = ls;
@@ -321,6 +361,7 @@ __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
 // ------------------------------------------------------------------------------------------------ actor step
 // update_actor's forward / backward (learner.py:138-175): loss = -mean Q1(s, actor(s)) with the updated critic.
 __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
+  __shared__ f4 sfrag[2 * 16 * 64];
   __shared__ float red[4 * H];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, j = lane & 15;
   const int64_t row = (int64_t)blockIdx.x * 64 + wave * 16 + j;
@@ -329,36 +370,36 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   const Net an = net_of(io.actor), qn = net_of(io.q1);
   float x[S1];
   input_frags(s_row, z4(), false, x, q);
-  if (q == 0) {
+  {
     float *xr = io.x0 + row * XP;
-    for (int f = 0; f < XP; ++f) xr[f] = f < 18 ? s_row[f] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int f = 8 * q + e;
+      xr[f] = f < 18 ? s_row[f] : 0.0f;
+    }
   }
   Tile h1, h2;
   gemm_in(an.f1(), x, h1, lane);
-  bias_tanh(h1, an.b1, q);
+  gemm256(an.fp(), h1, an.b1, h2, lane, sfrag);
   store_tile(io.h1, h1, row, q);
-  gemm256(an.fp(), h1, h2, lane);
-  bias_tanh(h2, an.b2, q);
+  const f4 pre = gemm_out(an.fo(), h2, an.b2, an.b3, 4, lane);
   store_tile(io.h2, h2, row, q);
-  const f4 pre = gemm_out(an.fo(), h2, an.b3, 4, lane);
   f4 a, au;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    a[c] = tanhf(pre[c]);
+    a[c] = tanh_fast(pre[c]);
     au[c] = unscale(a[c], io.act_low[c], io.act_range[c]);
   }
   // Q1(s, a)
   input_frags(s_row, au, true, x, q);
   gemm_in(qn.f1(), x, h1, lane);
-  bias_tanh(h1, qn.b1, q);
-  gemm256(qn.fp(), h1, h2, lane);
-  bias_tanh(h2, qn.b2, q);
-  const float qv = gemm_out(qn.fo(), h2, qn.b3, 1, lane)[0];
+  gemm256(qn.fp(), h1, qn.b1, h2, lane, sfrag);
+  const float qv = gemm_out(qn.fo(), h2, qn.b2, qn.b3, 1, lane)[0];
   const float g = -1.0f / (float)io.batch;  // d(-mean q) / dq
   Tile t;
   back_out(qn.w3, 1, f4{g, 0.0f, 0.0f, 0.0f}, t, q);
   tanh_back(t, h2);
-  gemm256(qn.bp(), t, h2, lane);
+  gemm256(qn.bp(), t, nullptr, h2, lane, sfrag);
   tanh_back(h2, h1);  // dz1 of Q1
   // dQ/d(unscaled action) = W1[:, 18:22]^T dz1, summed over the 4 lanes of the sample; then the unscale chain rule
   f4 da = z4();
@@ -390,62 +431,102 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   back_out(an.w3, 4, dz3, t, q);
   tanh_back(t, h2);
   store_tile(io.dz2, t, row, q);
-  wg_neuron_sum(t, red, io.p_db2 + (int64_t)blockIdx.x * H, wave, lane);
-  gemm256(an.bp(), t, h2, lane);
+  gemm256(an.bp(), t, nullptr, h2, lane, sfrag);
   load_tile(io.h1, h1, row, q);
   tanh_back(h2, h1);
   store_tile(io.dz1, h2, row, q);
-  wg_neuron_sum(h2, red, io.p_db1 + (int64_t)blockIdx.x * H, wave, lane);
   const float ls = wg_scalar_sum(-qv, red, wave, lane);
   if (threadIdx.x == 0) io.p_loss[blockIdx.x] = ls;
 }
 
 // ------------------------------------------------------------------------------------------------ weight gradients
 // dW[o][k] = sum_j DZ[j][o] X[j][k] over one chunk of CHUNK samples, o in 128-row tiles, k in KT-wide tiles; 4 waves
-// as 2 (o) x 2 (k).  The chunk streams through LDS 32 samples at a time.  Output: slab[chunk][256][ldx] (natural
-// W layout, fp32 partial sums; the adam kernel adds the chunks in order).
+// as 2 (o) x 2 (k).  The chunk streams through two LDS buffers 32 samples at a time (the next sub-chunk's loads are
+// in flight while the current one is multiplied).  Output: slab[chunk][256][ldx] (natural W layout, fp32 partial
+// sums; the adam kernel adds the chunks in order).  Blocks of the first k tile also sum DZ's columns: the bias
+// gradient partials bslab[chunk][256].  One launch runs up to 4 jobs (blockIdx.z = job * chunks + chunk).
+struct WgJob {
+  const float *dz, *x;
+  float *slab, *bslab;
+  int ldx;
+};
+struct WgJobs {
+  WgJob job[4];
+  int chunks;
+};
 template <int KT>
-__global__ void __launch_bounds__(WG, 1) wgrad_kernel(const float *__restrict__ dz, const float *__restrict__ xs, int ldx,
-                                                      float *__restrict__ slab) {
+__global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
   constexpr int SUB = 32, OT = 128, PAD = 4;
   constexpr int NB = KT == 128 ? 4 : 1;  // 16-column blocks per wave
-  __shared__ float sa[SUB][OT + PAD];
-  __shared__ float sb[SUB][KT + PAD];
+  constexpr int LA = SUB * OT / 4 / WG, LB = (SUB * KT / 4 + WG - 1) / WG;  // f4 loads per thread per sub-chunk
+  __shared__ float sa[2][SUB][OT + PAD];
+  __shared__ float sb[2][SUB][KT + PAD];
+  const int jb = blockIdx.z / jobs.chunks, chunk = blockIdx.z % jobs.chunks;
+  const float *__restrict__ dz = jobs.job[jb].dz;
+  const float *__restrict__ xs = jobs.job[jb].x;
+  float *__restrict__ slab = jobs.job[jb].slab;
+  float *__restrict__ bslab = jobs.job[jb].bslab;
+  const int ldx = jobs.job[jb].ldx;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, kk = lane >> 4, i = lane & 15;
   const int wo = wave >> 1, wk = wave & 1;
   const int o0 = blockIdx.x * OT, k0 = blockIdx.y * KT;
-  const int64_t j0 = (int64_t)blockIdx.z * CHUNK;
+  const int64_t j0 = (int64_t)chunk * CHUNK;
+  const bool bias = bslab != nullptr && blockIdx.y == 0;
   f4 acc[4][NB];
 #pragma unroll
   for (int bo = 0; bo < 4; ++bo)
 #pragma unroll
     for (int bk = 0; bk < NB; ++bk) acc[bo][bk] = z4();
-  for (int sub = 0; sub < CHUNK; sub += SUB) {
-    // stage DZ[j0 + sub .. +32][o0 .. o0 + 128] and X[..][k0 .. k0 + KT]
-    for (int e = threadIdx.x; e < SUB * OT / 4; e += WG) {
-      const int rr = e / (OT / 4), cc = (e % (OT / 4)) * 4;
-      *reinterpret_cast<f4 *>(&sa[rr][cc]) = *reinterpret_cast<const f4 *>(dz + (j0 + sub + rr) * H + o0 + cc);
+  float bsum = 0.0f;  // thread t < OT: column o0 + t of DZ
+  f4 ga[LA], gb[LB];
+  auto fetch = [&](int sub) {
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int e = threadIdx.x + u * WG, rr = e / (OT / 4), cc = (e % (OT / 4)) * 4;
+      ga[u] = *reinterpret_cast<const f4 *>(dz + (j0 + sub + rr) * H + o0 + cc);
     }
-    for (int e = threadIdx.x; e < SUB * KT / 4; e += WG) {
-      const int rr = e / (KT / 4), cc = (e % (KT / 4)) * 4;
-      *reinterpret_cast<f4 *>(&sb[rr][cc]) = *reinterpret_cast<const f4 *>(xs + (j0 + sub + rr) * ldx + k0 + cc);
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int e = threadIdx.x + u * WG, rr = e / (KT / 4), cc = (e % (KT / 4)) * 4;
+      if (e < SUB * KT / 4) gb[u] = *reinterpret_cast<const f4 *>(xs + (j0 + sub + rr) * ldx + k0 + cc);
     }
+  };
+  auto stash = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int e = threadIdx.x + u * WG, rr = e / (OT / 4), cc = (e % (OT / 4)) * 4;
+      *reinterpret_cast<f4 *>(&sa[b][rr][cc]) = ga[u];
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int e = threadIdx.x + u * WG, rr = e / (KT / 4), cc = (e % (KT / 4)) * 4;
+      if (e < SUB * KT / 4) *reinterpret_cast<f4 *>(&sb[b][rr][cc]) = gb[u];
+    }
+  };
+  fetch(0);
+  for (int sub = 0, b = 0; sub < CHUNK; sub += SUB, b ^= 1) {
+    stash(b);
     __syncthreads();
+    if (sub + SUB < CHUNK) fetch(sub + SUB);
+    if (bias && threadIdx.x < OT) {
+#pragma unroll
+      for (int r = 0; r < SUB; ++r) bsum += sa[b][r][threadIdx.x];
+    }
 #pragma unroll
     for (int s = 0; s < SUB / 4; ++s) {
-      const f4 A = *reinterpret_cast<const f4 *>(&sa[4 * s + kk][64 * wo + 4 * i]);  // rows o = 64 wo + 4 i + bo
+      const f4 A = *reinterpret_cast<const f4 *>(&sa[b][4 * s + kk][64 * wo + 4 * i]);  // rows o = 64 wo + 4 i + bo
       f4 B;
-      if constexpr (NB == 4) B = *reinterpret_cast<const f4 *>(&sb[4 * s + kk][64 * wk + 4 * i]);  // k = 64 wk + 4 i + bk
-      else B[0] = sb[4 * s + kk][16 * wk + i];                                                // k = 16 wk + i
+      if constexpr (NB == 4) B = *reinterpret_cast<const f4 *>(&sb[b][4 * s + kk][64 * wk + 4 * i]);  // k = 64 wk + 4 i + bk
+      else B[0] = sb[b][4 * s + kk][16 * wk + i];                                                // k = 16 wk + i
 #pragma unroll
       for (int bo = 0; bo < 4; ++bo)
 #pragma unroll
         for (int bk = 0; bk < NB; ++bk) acc[bo][bk] = mfma(A[bo], B[bk], acc[bo][bk]);
     }
-    __syncthreads();
   }
+  if (bias && threadIdx.x < OT) bslab[(int64_t)chunk * H + o0 + threadIdx.x] = bsum;
   // acc[bo][bk] lane (jj = i, q = kk) reg r: o = o0 + 64 wo + 4 (4 q + r) + bo, k = k0 + (NB == 4 ? 64 wk + 4 jj + bk : 16 wk + jj)
-  float *dst = slab + (int64_t)blockIdx.z * H * ldx;
+  float *dst = slab + (int64_t)chunk * H * ldx;
 #pragma unroll
   for (int bo = 0; bo < 4; ++bo)
 #pragma unroll
@@ -480,8 +561,14 @@ __global__ void __launch_bounds__(256) adam_kernel(hkl_adam_io io) {
     const int64_t k = e - base;
     const int64_t rr = k / S.cols, cc = k % S.cols;
     const float *src = S.src + rr * S.ld + cc;
-    float g = 0.0f;
-    for (int c = 0; c < S.chunks; ++c) g += src[(int64_t)c * S.stride];
+    float p8[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int c = 0;
+    for (; c + 8 <= S.chunks; c += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p8[u] += src[(int64_t)(c + u) * S.stride];
+    }
+    for (; c < S.chunks; ++c) p8[0] += src[(int64_t)c * S.stride];
+    float g = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
     float p = S.param[k];
     if (io.wd != 0.0f) g += io.wd * p;
     const float t = (float)(*io.step + 1);
@@ -509,6 +596,11 @@ __global__ void __launch_bounds__(256) polyak_kernel(float *__restrict__ t, cons
                                                      float tau) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e < n) t[e] = t[e] * rho + tau * p[e];
+}
+
+__global__ void tanh_probe_kernel(const float *x, float *y, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < n) y[e] = tanh_fast(x[e]);
 }
 
 // ------------------------------------------------------------------------------------------------ packing
@@ -583,13 +675,15 @@ int hkl_actor_step(const hkl_actor_io *io, void *stream) {
   return e == hipSuccess ? HKL_OK : fail(e, "hkl_actor_step");
 }
 
-int hkl_wgrad(const float *dz, const float *x, int k_width, int64_t batch, float *slab, void *stream) {
-  if (batch <= 0 || batch % CHUNK || (k_width != 256 && k_width != XP)) return HKL_E_INVALID;
-  const unsigned chunks = (unsigned)(batch / CHUNK);
-  if (k_width == 256)
-    hipLaunchKernelGGL(wgrad_kernel<128>, dim3(2, 2, chunks), dim3(WG), 0, (hipStream_t)stream, dz, x, 256, slab);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<32>, dim3(2, 1, chunks), dim3(WG), 0, (hipStream_t)stream, dz, x, XP, slab);
+int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch, void *stream) {
+  if (!jobs || n_jobs < 1 || n_jobs > 4 || batch <= 0 || batch % CHUNK || (k_width != 256 && k_width != XP))
+    return HKL_E_INVALID;
+  WgJobs J{};
+  for (int k = 0; k < n_jobs; ++k) J.job[k] = WgJob{jobs[k].dz, jobs[k].x, jobs[k].slab, jobs[k].bias_slab, k_width};
+  J.chunks = (int)(batch / CHUNK);
+  const unsigned z = (unsigned)(J.chunks * n_jobs);
+  if (k_width == 256) hipLaunchKernelGGL(wgrad_kernel<128>, dim3(2, 2, z), dim3(WG), 0, (hipStream_t)stream, J);
+  else hipLaunchKernelGGL(wgrad_kernel<32>, dim3(2, 1, z), dim3(WG), 0, (hipStream_t)stream, J);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? HKL_OK : fail(e, "hkl_wgrad");
 }
@@ -612,5 +706,12 @@ int hkl_polyak(float *target, const float *param, int64_t n, float rho, float ta
 }
 
 int hkl_pack_floats(void) { return kPackFloats; }
+
+int hkl_tanh_probe(const float *x, float *y, int64_t n, void *stream) {
+  if (n <= 0) return HKL_E_INVALID;
+  hipLaunchKernelGGL(tanh_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, y, n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? HKL_OK : fail(e, "hkl_tanh_probe");
+}
 
 }  // extern "C"

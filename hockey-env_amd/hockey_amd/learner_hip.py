@@ -52,6 +52,10 @@ class ActorIO(ctypes.Structure):
                 ("p_loss", vp)]
 
 
+class WgJob(ctypes.Structure):
+    _fields_ = [("dz", vp), ("x", vp), ("slab", vp), ("bias_slab", vp)]
+
+
 class Seg(ctypes.Structure):
     _fields_ = [("param", vp), ("m", vp), ("v", vp), ("src", vp), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
                 ("ld", ctypes.c_int64), ("chunks", ctypes.c_int32), ("stride", ctypes.c_int64)]
@@ -65,7 +69,16 @@ class AdamIO(ctypes.Structure):
 
 
 EXPORTS = ["hkl_last_error", "hkl_pack_floats", "hkl_pack", "hkl_critic_step", "hkl_actor_step", "hkl_wgrad",
-           "hkl_adam", "hkl_polyak"]
+           "hkl_adam", "hkl_polyak", "hkl_tanh_probe"]
+
+
+def tanh_probe(x):
+    """The fused kernels' tanh of a device float32 tensor (accuracy check)."""
+    x = x.contiguous().float()
+    y = torch.empty_like(x)
+    _check(lib().hkl_tanh_probe(_p(x), _p(y), x.numel(),
+                                ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)), "hkl_tanh_probe")
+    return y
 _lib = None
 
 
@@ -81,9 +94,10 @@ def lib():
         L.hkl_pack.argtypes = [ctypes.POINTER(Net), ctypes.c_int, vp, vp]
         L.hkl_critic_step.argtypes = [ctypes.POINTER(CriticIO), vp]
         L.hkl_actor_step.argtypes = [ctypes.POINTER(ActorIO), vp]
-        L.hkl_wgrad.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int64, vp, vp]
+        L.hkl_wgrad.argtypes = [ctypes.POINTER(WgJob), ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp]
         L.hkl_adam.argtypes = [ctypes.POINTER(AdamIO), vp]
         L.hkl_polyak.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_float, ctypes.c_float, vp]
+        L.hkl_tanh_probe.argtypes = [vp, vp, ctypes.c_int64, vp]
         if L.hkl_pack_floats() != PACK_FLOATS:
             raise _native.HockeyNativeError("libhockey_learner.so pack size differs from hockey_amd.learner_hip")
         _lib = L
@@ -165,7 +179,9 @@ class FusedLearner:
         self.buf["pa_dw3"], self.buf["pa_db3"] = z(G, 4, 256), z(G, 4)
         self.buf["s_w2"] = [z(C, 256, 256), z(C, 256, 256)]
         self.buf["s_w1"] = [z(C, 256, XP), z(C, 256, XP)]
+        self.buf["s_b2"], self.buf["s_b1"] = [z(C, 256), z(C, 256)], [z(C, 256), z(C, 256)]
         self.buf["sa_w2"], self.buf["sa_w1"] = z(C, 256, 256), z(C, 256, XP)
+        self.buf["sa_b2"], self.buf["sa_b1"] = z(C, 256), z(C, 256)
         self.idx = torch.zeros(B, dtype=torch.int64, device=dev)
         self.iw = z(B) if ring.prioritized else None
         low = agent.critic.action_low.float().cpu().tolist()
@@ -218,11 +234,11 @@ class FusedLearner:
             for key, k in nets:
                 f1, f2, f3 = _mlp_layers(n[key].m)
                 if k is None:
-                    srcs = [(b["sa_w1"], XP, C, 256 * XP), (b["pa_db1"], 256, G, 256), (b["sa_w2"], 256, C, 65536),
-                            (b["pa_db2"], 256, G, 256), (b["pa_dw3"], 256, G, 1024), (b["pa_db3"], 4, G, 4)]
+                    srcs = [(b["sa_w1"], XP, C, 256 * XP), (b["sa_b1"], 256, C, 256), (b["sa_w2"], 256, C, 65536),
+                            (b["sa_b2"], 256, C, 256), (b["pa_dw3"], 256, G, 1024), (b["pa_db3"], 4, G, 4)]
                 else:
-                    srcs = [(b["s_w1"][k], XP, C, 256 * XP), (b["p_db1"][k], 256, G, 256), (b["s_w2"][k], 256, C, 65536),
-                            (b["p_db2"][k], 256, G, 256), (b["p_dw3"][k], 256, G, 256), (b["p_db3"][k], 1, G, 1)]
+                    srcs = [(b["s_w1"][k], XP, C, 256 * XP), (b["s_b1"][k], 256, C, 256), (b["s_w2"][k], 256, C, 65536),
+                            (b["s_b2"][k], 256, C, 256), (b["p_dw3"][k], 256, G, 256), (b["p_db3"][k], 1, G, 1)]
                 for p, (src, ld, chunks, stride) in zip((f1.weight, f1.bias, f2.weight, f2.bias, f3.weight, f3.bias),
                                                         srcs):
                     rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.shape[0])
@@ -240,6 +256,12 @@ class FusedLearner:
             io.loss_chunks = G
             io.loss_scale = (0.5 if name == "critic" else 1.0) / self.B
             self.adam[name] = io
+        # weight-gradient jobs (one launch per k width): critics' dW2 / dW1 (+ b2 / b1), actor's
+        J = lambda dz, x, sl, bs: WgJob(_p(dz), _p(x), _p(sl), _p(bs))  # noqa: E731
+        self.wg = {"c256": (WgJob * 2)(*[J(b["dz2"][k], b["h1"][k], b["s_w2"][k], b["s_b2"][k]) for k in range(2)]),
+                   "c32": (WgJob * 2)(*[J(b["dz1"][k], b["x0"], b["s_w1"][k], b["s_b1"][k]) for k in range(2)]),
+                   "a256": (WgJob * 1)(J(b["dz2a"], b["h1a"], b["sa_w2"], b["sa_b2"])),
+                   "a32": (WgJob * 1)(J(b["dz1a"], b["x0a"], b["sa_w1"], b["sa_b1"]))}
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.agent.device).cuda_stream)
@@ -273,9 +295,8 @@ class FusedLearner:
             noise = torch.randn((self.B, 4), device=self.agent.device) * c.target_action_noise_scale
         b["noise"].copy_(torch.clamp(noise, -c.target_action_noise_clip, c.target_action_noise_clip))
         _check(L.hkl_critic_step(ctypes.byref(self.cio), st), "hkl_critic_step")
-        for k in range(2):
-            _check(L.hkl_wgrad(_p(b["dz2"][k]), _p(b["h1"][k]), 256, self.B, _p(b["s_w2"][k]), st), "hkl_wgrad")
-            _check(L.hkl_wgrad(_p(b["dz1"][k]), _p(b["x0"]), XP, self.B, _p(b["s_w1"][k]), st), "hkl_wgrad")
+        _check(L.hkl_wgrad(self.wg["c256"], 2, 256, self.B, st), "hkl_wgrad")
+        _check(L.hkl_wgrad(self.wg["c32"], 2, XP, self.B, st), "hkl_wgrad")
         _check(L.hkl_adam(ctypes.byref(self.adam["critic"]), st), "hkl_adam")
         self._pack([self.nets["q1"], self.nets["q2"]], self.step["critic"], st)
         if self.ring.prioritized:
@@ -284,8 +305,8 @@ class FusedLearner:
         if not train_actor:
             return
         _check(L.hkl_actor_step(ctypes.byref(self.aio), st), "hkl_actor_step")
-        _check(L.hkl_wgrad(_p(b["dz2a"]), _p(b["h1a"]), 256, self.B, _p(b["sa_w2"]), st), "hkl_wgrad")
-        _check(L.hkl_wgrad(_p(b["dz1a"]), _p(b["x0a"]), XP, self.B, _p(b["sa_w1"]), st), "hkl_wgrad")
+        _check(L.hkl_wgrad(self.wg["a256"], 1, 256, self.B, st), "hkl_wgrad")
+        _check(L.hkl_wgrad(self.wg["a32"], 1, XP, self.B, st), "hkl_wgrad")
         _check(L.hkl_adam(ctypes.byref(self.adam["actor"]), st), "hkl_adam")
         self._pack([self.nets["actor"]], self.step["actor"], st)
         ta, tc = c.tau_actor, c.tau_critic

@@ -33,7 +33,8 @@ typedef struct {
  * (s [cap][18], a [cap][4], r [cap], s2 [cap][18], d [cap]), the sampled slots idx [B], the clipped target noise
  * [B][4], optional importance weights iw [B].  Outputs: X0 [B][32] (critic inputs), per critic k: H1, DZ1, DZ2
  * [B][256]; workgroup partials (B / 64 rows) of db1, db2, dW3 [.][256] and db3 [.]; loss partials [B / 64];
- * optional td [B] = (|q1 - y| + |q2 - y|) / 2 for prioritized replay. */
+ * optional td [B] = (|q1 - y| + |q2 - y|) / 2 for prioritized replay.  (db1 / db2 come from hkl_wgrad's
+ * column sums; p_db1 / p_db2 are unused.) */
 typedef struct {
   int64_t batch;
   const int64_t *idx;
@@ -48,8 +49,8 @@ typedef struct {
 } hkl_critic_io;
 
 /* update_actor forward / backward: actor(s), Q1(s, actor(s)) of the updated critic, d(-mean Q1).  Outputs: X0
- * [B][32], H1, H2, DZ1, DZ2 [B][256]; workgroup partials of db1, db2 [.][256], dW3 [.][4][256], db3 [.][4];
- * loss partials. */
+ * [B][32], H1, H2, DZ1, DZ2 [B][256]; workgroup partials of dW3 [.][4][256], db3 [.][4]; loss partials
+ * (p_db1 / p_db2 unused). */
 typedef struct {
   int64_t batch;
   const int64_t *idx;
@@ -93,11 +94,20 @@ int hkl_pack_floats(void);
 int hkl_pack(const hkl_net *nets, int n_nets, int64_t *step, void *stream);
 int hkl_critic_step(const hkl_critic_io *io, void *stream);
 int hkl_actor_step(const hkl_actor_io *io, void *stream);
-/* slab[c][256][k_width] = sum over samples of chunk c (256 each) of dz[j][o] x[j][k]; k_width 256 or 32 */
-int hkl_wgrad(const float *dz, const float *x, int k_width, int64_t batch, float *slab, void *stream);
+/* weight-gradient job: slab[c][256][k_width] = sum over the samples j of chunk c (256 each) of dz[j][o] x[j][k]
+ * (dz [B][256], x [B][k_width]); bias_slab (optional) [c][256] = the chunk's column sums of dz */
+typedef struct {
+  const float *dz, *x;
+  float *slab, *bias_slab;
+} hkl_wgrad_job;
+/* 1..4 jobs of one k_width (256 or 32) in one launch */
+int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch, void *stream);
 int hkl_adam(const hkl_adam_io *io, void *stream);
 /* target = target * rho + tau * param over n floats (soft_update; tau = 1 - rho) */
 int hkl_polyak(float *target, const float *param, int64_t n, float rho, float tau, void *stream);
+
+/* y = the kernels' tanh of x (n floats; a test probe of the activation's accuracy) */
+int hkl_tanh_probe(const float *x, float *y, int64_t n, void *stream);
 
 #ifdef __cplusplus
 }

@@ -159,3 +159,12 @@ def test_fused_graph_replay_equals_fused_eager():
                                list(agent.critic.parameters()) + list(agent.target_actor.parameters()) +
                                list(agent.target_critic.parameters())]))
     assert torch.equal(nets[0], nets[1]), (nets[0] - nets[1]).abs().max()
+
+
+def test_fused_tanh_accuracy():
+    """The fused kernels' branch-free tanh against torch.tanh over [-20, 20] and near 0: |error| < 2e-7."""
+    from hockey_amd.learner_hip import tanh_probe
+
+    x = torch.cat([torch.linspace(-20, 20, 1_000_001, device=DEV), torch.linspace(-1e-3, 1e-3, 100_001, device=DEV)])
+    err = (tanh_probe(x).double() - torch.tanh(x.double())).abs().max().item()
+    assert err < 2e-7, err
