@@ -30,7 +30,7 @@ constexpr int H = 256;   // hidden width (rl/td3/networks.py: h = 256)
 constexpr int XP = 32;   // padded row of the stored first-layer inputs X0 [B][XP]
 constexpr int S1 = 6;    // first-layer k-steps: inputs padded to 24
 constexpr int WG = 256;  // threads of the fused kernels: 4 waves x 16 samples = 64 samples per workgroup
-constexpr int CHUNK = 256;  // samples per split-K chunk of the weight-gradient kernel
+constexpr int CHUNK = 256;  // batch granularity; the weight-gradient kernel's split-K chunks are 256 or 512 samples
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -101,6 +101,8 @@ __device__ __forceinline__ void gemm_in(const float *__restrict__ f1, const floa
 __device__ __forceinline__ void gemm256(const f4 *__restrict__ P, Tile &in, const float *__restrict__ bias, Tile &out,
                                         int lane, f4 *sfrag) {
   const int wave = threadIdx.x >> 6, q = lane >> 4;
+  float *sbias = reinterpret_cast<float *>(sfrag + 2 * 1024);  // the bias, staged once (no global wait per k-block)
+  if (bias) sbias[threadIdx.x] = bias[threadIdx.x];
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) out.v[ob] = z4();
   f4 g[4];
@@ -120,7 +122,7 @@ __device__ __forceinline__ void gemm256(const f4 *__restrict__ P, Tile &in, cons
 #pragma unroll
     for (int ob = 0; ob < 16; ++ob) a[ob] = buf[ob * 64 + lane];
     if (bias) {
-      const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * kb + 4 * q);
+      const f4 bb = *reinterpret_cast<const f4 *>(sbias + 16 * kb + 4 * q);
 #pragma unroll
       for (int r = 0; r < 4; ++r) in.v[kb][r] = tanh_fast(in.v[kb][r] + bb[r]);
     }
@@ -149,17 +151,23 @@ __device__ __forceinline__ void bias_tanh(Tile &t, const float *__restrict__ b, 
   }
 }
 
-// the n_out (<= 4) outputs W3 h + b3 of this lane's sample, broadcast to every lane of the sample.  bias !=
+// the n_out (<= 4) outputs W3 h + b3 of this lane's sample, broadcast to every lane of the sample; a
+// workgroup-collective call (the W3 fragments and the bias are staged in LDS once for the 4 waves).  bias !=
 // nullptr: h holds pre-activations, activated in place (tanh(h + bias)) block by block as in gemm256.
 __device__ __forceinline__ f4 gemm_out(const f4 *__restrict__ fo, Tile &h, const float *__restrict__ bias,
-                                       const float *__restrict__ b3, int n_out, int lane) {
+                                       const float *__restrict__ b3, int n_out, int lane, f4 *sfrag) {
   const int q = lane >> 4;
+  float *sbias = reinterpret_cast<float *>(sfrag + 2 * 1024);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sfrag[threadIdx.x + i * WG] = fo[threadIdx.x + i * WG];
+  if (bias) sbias[threadIdx.x] = bias[threadIdx.x];
+  __syncthreads();
   f4 acc0 = z4(), acc1 = z4();
 #pragma unroll
   for (int kb = 0; kb < 16; ++kb) {
-    const f4 a = fo[kb * 64 + lane];
+    const f4 a = sfrag[kb * 64 + lane];
     if (bias) {
-      const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * kb + 4 * q);
+      const f4 bb = *reinterpret_cast<const f4 *>(sbias + 16 * kb + 4 * q);
 #pragma unroll
       for (int r = 0; r < 4; ++r) h.v[kb][r] = tanh_fast(h.v[kb][r] + bb[r]);
     }
@@ -169,6 +177,7 @@ __device__ __forceinline__ f4 gemm_out(const f4 *__restrict__ fo, Tile &h, const
       else acc0 = mfma(a[r], h.v[kb][r], acc0);
     }
   }
+  __syncthreads();  // the staging buffers are reused by the next collective call
   const f4 acc = acc0 + acc1;  // lanes 0..15 hold outputs 0..3 of sample lane & 15
   f4 o;
 #pragma unroll
@@ -270,7 +279,7 @@ __device__ __forceinline__ float q_forward(const Net &c, const float (&x)[S1], T
                                            f4 *sfrag) {
   gemm_in(c.f1(), x, h1, lane);
   gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
-  return gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane)[0];
+  return gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane, sfrag)[0];
 }
 
 // one critic k of update_critic: forward on x, the weighted smooth-L1 (torch_utils.py:12-24; critic_loss =
@@ -283,7 +292,7 @@ __device__ __forceinline__ void critic_one(const hkl_critic_io &io, int k, const
   gemm_in(c.f1(), x, h1, lane);
   gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
   store_tile(io.h1[k], h1, row, q);
-  const float qv = gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane)[0];
+  const float qv = gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane, sfrag)[0];
   const float diff = qv - y, ad = fabsf(diff);
   loss += ad < 1.0f ? 0.5f * w * diff * diff : (ad - 0.5f) * w;
   const float g = (ad < 1.0f ? w * diff : (diff > 0.0f ? w : diff < 0.0f ? -w : 0.0f)) * (0.5f / (float)io.batch);
@@ -307,7 +316,7 @@ __device__ __forceinline__ void critic_one(const hkl_critic_io &io, int k, const
 
 // compute_target + update_critic's forward / loss / backward for both critics (learner.py:75-136).
 __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
-  __shared__ f4 sfrag[2 * 16 * 64];
+  __shared__ f4 sfrag[2 * 16 * 64 + 64];  // two fragment buffers + the staged bias
   __shared__ float red[4 * H];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, j = lane & 15;
   const int64_t row = (int64_t)blockIdx.x * 64 + wave * 16 + j;  // this lane's sample (batch row)
@@ -326,7 +335,7 @@ __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
   Tile h1, h2;
   gemm_in(ta.f1(), x, h1, lane);
   gemm256(ta.fp(), h1, ta.b1, h2, lane, sfrag);
-  const f4 a2 = gemm_out(ta.fo(), h2, ta.b2, ta.b3, 4, lane);
+  const f4 a2 = gemm_out(ta.fo(), h2, ta.b2, ta.b3, 4, lane, sfrag);
   f4 a2u;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -356,12 +365,13 @@ __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
   if (io.td && q == 0) io.td[row] = td * 0.5f;  // (|q1 - y| + |q2 - y|) / 2 (learner.py:163-170)
   const float ls = wg_scalar_sum(loss, red, wave, lane);
   if (threadIdx.x == 0) io.p_loss[blockIdx.x] = ls;
+  if (io.sample_counter && blockIdx.x == 0 && threadIdx.x == 0) *io.sample_counter += 1;
 }
 
 // ------------------------------------------------------------------------------------------------ actor step
 // update_actor's forward / backward (learner.py:138-175): loss = -mean Q1(s, actor(s)) with the updated critic.
 __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
-  __shared__ f4 sfrag[2 * 16 * 64];
+  __shared__ f4 sfrag[2 * 16 * 64 + 64];  // two fragment buffers + the staged bias
   __shared__ float red[4 * H];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, j = lane & 15;
   const int64_t row = (int64_t)blockIdx.x * 64 + wave * 16 + j;
@@ -382,7 +392,7 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   gemm_in(an.f1(), x, h1, lane);
   gemm256(an.fp(), h1, an.b1, h2, lane, sfrag);
   store_tile(io.h1, h1, row, q);
-  const f4 pre = gemm_out(an.fo(), h2, an.b2, an.b3, 4, lane);
+  const f4 pre = gemm_out(an.fo(), h2, an.b2, an.b3, 4, lane, sfrag);
   store_tile(io.h2, h2, row, q);
   f4 a, au;
 #pragma unroll
@@ -394,7 +404,7 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   input_frags(s_row, au, true, x, q);
   gemm_in(qn.f1(), x, h1, lane);
   gemm256(qn.fp(), h1, qn.b1, h2, lane, sfrag);
-  const float qv = gemm_out(qn.fo(), h2, qn.b2, qn.b3, 1, lane)[0];
+  const float qv = gemm_out(qn.fo(), h2, qn.b2, qn.b3, 1, lane, sfrag)[0];
   const float g = -1.0f / (float)io.batch;  // d(-mean q) / dq
   Tile t;
   back_out(qn.w3, 1, f4{g, 0.0f, 0.0f, 0.0f}, t, q);
@@ -452,7 +462,7 @@ struct WgJob {
 };
 struct WgJobs {
   WgJob job[4];
-  int chunks;
+  int chunks, chunk_size;
 };
 template <int KT>
 __global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
@@ -470,7 +480,8 @@ __global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, kk = lane >> 4, i = lane & 15;
   const int wo = wave >> 1, wk = wave & 1;
   const int o0 = blockIdx.x * OT, k0 = blockIdx.y * KT;
-  const int64_t j0 = (int64_t)chunk * CHUNK;
+  const int csize = jobs.chunk_size;
+  const int64_t j0 = (int64_t)chunk * csize;
   const bool bias = bslab != nullptr && blockIdx.y == 0;
   f4 acc[4][NB];
 #pragma unroll
@@ -504,10 +515,10 @@ __global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
     }
   };
   fetch(0);
-  for (int sub = 0, b = 0; sub < CHUNK; sub += SUB, b ^= 1) {
+  for (int sub = 0, b = 0; sub < csize; sub += SUB, b ^= 1) {
     stash(b);
     __syncthreads();
-    if (sub + SUB < CHUNK) fetch(sub + SUB);
+    if (sub + SUB < csize) fetch(sub + SUB);
     if (bias && threadIdx.x < OT) {
 #pragma unroll
       for (int r = 0; r < SUB; ++r) bsum += sa[b][r][threadIdx.x];
@@ -598,6 +609,54 @@ __global__ void __launch_bounds__(256) polyak_kernel(float *__restrict__ t, cons
   if (e < n) t[e] = t[e] * rho + tau * p[e];
 }
 
+// ------------------------------------------------------------------------------------------------ sampling
+// The batch's replay slots and target noise from a counter-based RNG (Philox4x32-10 keyed by the learner's seed, the
+// counter = (sample, update, purpose)): uniform slots floor(u * size) with a 53-bit u (rl/replay/uniform_buffer.py's
+// (rand * size).astype(int)), and the target policy smoothing noise clamp(N(0, scale), -clip, clip) by Box-Muller
+// (learner.py:80-93).  The update counter lives in device memory (graph replays advance it): critic_step bumps it.
+struct P4 {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ P4 philox(uint64_t key, P4 c) {
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = P4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__global__ void __launch_bounds__(256) sample_kernel(hkl_sample_io io) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= io.batch) return;
+  const uint64_t ctr = (uint64_t)*io.counter, size = (uint64_t)*io.size;
+  const P4 r0 = philox(io.seed, P4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32)});
+  const uint64_t bits = (((uint64_t)r0.x << 32) | r0.y) >> 11;
+  const double u = (double)bits * (1.0 / 9007199254740992.0);
+  const uint64_t i = (uint64_t)(u * (double)size);
+  io.idx[e] = (int64_t)(i < size ? i : size - 1);
+  const P4 r1 = philox(io.seed ^ 0x6E6F697365ull, P4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32)});
+  const uint32_t w[4] = {r1.x, r1.y, r1.z, r1.w};
+  float z[4];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float u1 = ((float)(w[2 * p] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+    const float u2 = (float)(w[2 * p + 1] >> 8) * (1.0f / 16777216.0f);
+    const float rad = sqrtf(-2.0f * logf(u1));
+    float sn, cs;
+    sincosf(6.283185307179586f * u2, &sn, &cs);
+    z[2 * p] = rad * cs;
+    z[2 * p + 1] = rad * sn;
+  }
+  f4 nz;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) nz[c] = fminf(fmaxf(z[c] * io.scale, -io.clip), io.clip);
+  *reinterpret_cast<f4 *>(io.noise + e * 4) = nz;
+}
+
 __global__ void tanh_probe_kernel(const float *x, float *y, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e < n) y[e] = tanh_fast(x[e]);
@@ -680,7 +739,10 @@ int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch,
     return HKL_E_INVALID;
   WgJobs J{};
   for (int k = 0; k < n_jobs; ++k) J.job[k] = WgJob{jobs[k].dz, jobs[k].x, jobs[k].slab, jobs[k].bias_slab, k_width};
-  J.chunks = (int)(batch / CHUNK);
+  // dW2 (k width 256): 512-sample chunks when the batch allows (fewer partial slabs for adam to add); dW1 (k width
+  // 32, a small tile per block): 256, for more blocks
+  J.chunk_size = (k_width == 256 && batch % 512 == 0) ? 512 : 256;
+  J.chunks = (int)(batch / J.chunk_size);
   const unsigned z = (unsigned)(J.chunks * n_jobs);
   if (k_width == 256) hipLaunchKernelGGL(wgrad_kernel<128>, dim3(2, 2, z), dim3(WG), 0, (hipStream_t)stream, J);
   else hipLaunchKernelGGL(wgrad_kernel<32>, dim3(2, 1, z), dim3(WG), 0, (hipStream_t)stream, J);
@@ -706,6 +768,13 @@ int hkl_polyak(float *target, const float *param, int64_t n, float rho, float ta
 }
 
 int hkl_pack_floats(void) { return kPackFloats; }
+
+int hkl_sample(const hkl_sample_io *io, void *stream) {
+  if (!io || io->batch <= 0) return HKL_E_INVALID;
+  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((io->batch + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *io);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? HKL_OK : fail(e, "hkl_sample");
+}
 
 int hkl_tanh_probe(const float *x, float *y, int64_t n, void *stream) {
   if (n <= 0) return HKL_E_INVALID;

@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("HK_LEARNER_LIB") or os.path.join(os.path.dirname(os.p
                                                             "libhockey_learner.so")
 PACK_FLOATS = 16 * 64 * 8 + 2 * 16 * 16 * 64 * 4 + 16 * 64 * 4 + 256 * 4
 MAX_SEG = 12
-CHUNK = 256
+CHUNK = 256  # batch granularity (include/hockey_learner.h)
 XP = 32
 
 vp = ctypes.c_void_p
@@ -42,7 +42,12 @@ class CriticIO(ctypes.Structure):
                 ("target_q", Net * 2), ("q", Net * 2), ("gamma", ctypes.c_float), ("act_low", ctypes.c_float * 4),
                 ("act_range", ctypes.c_float * 4), ("x0", vp), ("h1", vp * 2), ("dz1", vp * 2), ("dz2", vp * 2),
                 ("p_db1", vp * 2), ("p_db2", vp * 2), ("p_dw3", vp * 2), ("p_db3", vp * 2), ("p_loss", vp),
-                ("td", vp)]
+                ("td", vp), ("sample_counter", vp)]
+
+
+class SampleIO(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int64), ("seed", ctypes.c_uint64), ("counter", vp), ("size", vp), ("idx", vp),
+                ("noise", vp), ("scale", ctypes.c_float), ("clip", ctypes.c_float)]
 
 
 class ActorIO(ctypes.Structure):
@@ -69,7 +74,7 @@ class AdamIO(ctypes.Structure):
 
 
 EXPORTS = ["hkl_last_error", "hkl_pack_floats", "hkl_pack", "hkl_critic_step", "hkl_actor_step", "hkl_wgrad",
-           "hkl_adam", "hkl_polyak", "hkl_tanh_probe"]
+           "hkl_adam", "hkl_polyak", "hkl_tanh_probe", "hkl_sample"]
 
 
 def tanh_probe(x):
@@ -98,6 +103,7 @@ def lib():
         L.hkl_adam.argtypes = [ctypes.POINTER(AdamIO), vp]
         L.hkl_polyak.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_float, ctypes.c_float, vp]
         L.hkl_tanh_probe.argtypes = [vp, vp, ctypes.c_int64, vp]
+        L.hkl_sample.argtypes = [ctypes.POINTER(SampleIO), vp]
         if L.hkl_pack_floats() != PACK_FLOATS:
             raise _native.HockeyNativeError("libhockey_learner.so pack size differs from hockey_amd.learner_hip")
         _lib = L
@@ -145,8 +151,11 @@ class FusedLearner:
     """Learner updates of ``agent`` (hockey_amd.td3.TD3) on ``ring`` at batch ``batch`` (a multiple of 256) with the
     fused kernels; same interface as the eager path: ``update(train_actor, acc)``."""
 
-    def __init__(self, agent, ring, batch):
+    def __init__(self, agent, ring, batch, rng="device", seed=None):
         L = lib()
+        if rng not in ("device", "torch"):
+            raise ValueError("rng must be 'device' or 'torch'")
+        self.rng = rng
         self.L = L
         self.agent, self.ring, self.B = agent, ring, int(batch)
         dev = agent.device
@@ -156,7 +165,9 @@ class FusedLearner:
             raise ValueError(f"fused learner batch must be a positive multiple of {CHUNK}, got {self.B}")
         if agent.actor.fc1.out_features != 256:
             raise ValueError("fused learner: hidden width 256 only (rl/td3/networks.py h)")
-        B, G, C = self.B, self.B // 64, self.B // CHUNK
+        B, G = self.B, self.B // 64
+        C = self.B // (512 if self.B % 512 == 0 else 256)  # hkl_wgrad's split-K chunks: dW2 (k width 256)
+        C1 = self.B // 256  # dW1 (k width 32)
         c = agent.cfg
         self.cfg = c
         self.flat = {k: flatten_(getattr(agent, k)) for k in ("actor", "critic", "target_actor", "target_critic")}
@@ -178,11 +189,19 @@ class FusedLearner:
         self.buf["pa_db1"], self.buf["pa_db2"] = z(G, 256), z(G, 256)
         self.buf["pa_dw3"], self.buf["pa_db3"] = z(G, 4, 256), z(G, 4)
         self.buf["s_w2"] = [z(C, 256, 256), z(C, 256, 256)]
-        self.buf["s_w1"] = [z(C, 256, XP), z(C, 256, XP)]
-        self.buf["s_b2"], self.buf["s_b1"] = [z(C, 256), z(C, 256)], [z(C, 256), z(C, 256)]
-        self.buf["sa_w2"], self.buf["sa_w1"] = z(C, 256, 256), z(C, 256, XP)
-        self.buf["sa_b2"], self.buf["sa_b1"] = z(C, 256), z(C, 256)
+        self.buf["s_w1"] = [z(C1, 256, XP), z(C1, 256, XP)]
+        self.buf["s_b2"], self.buf["s_b1"] = [z(C, 256), z(C, 256)], [z(C1, 256), z(C1, 256)]
+        self.buf["sa_w2"], self.buf["sa_w1"] = z(C, 256, 256), z(C1, 256, XP)
+        self.buf["sa_b2"], self.buf["sa_b1"] = z(C, 256), z(C1, 256)
         self.idx = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.sample_counter = torch.zeros((), dtype=torch.int64, device=dev)
+        sio = SampleIO()
+        sio.batch = B
+        sio.seed = (int(agent.seed if seed is None else seed) * 0x9E3779B97F4A7C15 + 0x4C4541524E) % (1 << 64)
+        sio.counter, sio.size, sio.idx, sio.noise = (_p(self.sample_counter), _p(ring.size_t), _p(self.idx),
+                                                     _p(self.buf["noise"]))
+        sio.scale, sio.clip = c.target_action_noise_scale, c.target_action_noise_clip
+        self.sio = sio
         self.iw = z(B) if ring.prioritized else None
         low = agent.critic.action_low.float().cpu().tolist()
         rng = agent.critic.action_range.float().cpu().tolist()
@@ -211,6 +230,7 @@ class FusedLearner:
             cio.p_db1[k], cio.p_db2[k] = _p(b["p_db1"][k]), _p(b["p_db2"][k])
             cio.p_dw3[k], cio.p_db3[k] = _p(b["p_dw3"][k]), _p(b["p_db3"][k])
         cio.p_loss, cio.td = _p(b["loss_c"]), _p(b["td"])
+        cio.sample_counter = _p(self.sample_counter)
         self.cio = cio
         aio = ActorIO()
         aio.batch, aio.idx, aio.ring_s = self.B, _p(self.idx), _p(r.s)
@@ -222,7 +242,7 @@ class FusedLearner:
         aio.p_db1, aio.p_db2, aio.p_dw3, aio.p_db3 = _p(b["pa_db1"]), _p(b["pa_db2"]), _p(b["pa_dw3"]), _p(b["pa_db3"])
         aio.p_loss = _p(b["loss_a"])
         self.aio = aio
-        G, C = self.B // 64, self.B // CHUNK
+        G, C, C1 = self.B // 64, self.B // (512 if self.B % 512 == 0 else 256), self.B // 256
         # Adam segments: torch parameter order of each network (fc1.w, fc1.b, fc2.w, fc2.b, fc3.w, fc3.b)
         self.adam = {}
         for name, nets, lr, wd in (("critic", [("q1", 0), ("q2", 1)], self.cfg.lr_q, self.cfg.wd_q),
@@ -234,10 +254,10 @@ class FusedLearner:
             for key, k in nets:
                 f1, f2, f3 = _mlp_layers(n[key].m)
                 if k is None:
-                    srcs = [(b["sa_w1"], XP, C, 256 * XP), (b["sa_b1"], 256, C, 256), (b["sa_w2"], 256, C, 65536),
+                    srcs = [(b["sa_w1"], XP, C1, 256 * XP), (b["sa_b1"], 256, C1, 256), (b["sa_w2"], 256, C, 65536),
                             (b["sa_b2"], 256, C, 256), (b["pa_dw3"], 256, G, 1024), (b["pa_db3"], 4, G, 4)]
                 else:
-                    srcs = [(b["s_w1"][k], XP, C, 256 * XP), (b["s_b1"][k], 256, C, 256), (b["s_w2"][k], 256, C, 65536),
+                    srcs = [(b["s_w1"][k], XP, C1, 256 * XP), (b["s_b1"][k], 256, C1, 256), (b["s_w2"][k], 256, C, 65536),
                             (b["s_b2"][k], 256, C, 256), (b["p_dw3"][k], 256, G, 256), (b["p_db3"][k], 1, G, 1)]
                 for p, (src, ld, chunks, stride) in zip((f1.weight, f1.bias, f2.weight, f2.bias, f3.weight, f3.bias),
                                                         srcs):
@@ -280,20 +300,27 @@ class FusedLearner:
     # ------------------------------------------------------------------ one update
     def update(self, train_actor, idx=None, noise=None):
         """learner.update on a batch sampled from the ring: critic step, then (train_actor) the actor step and the
-        Polyak averaging of both targets.  idx / noise (tests): the batch's ring slots and the UNCLIPPED N(0, scale)
-        target noise [B, 4] to use instead of drawing them."""
+        Polyak averaging of both targets.  The batch's slots and target noise come from the device Philox stream
+        (rng="device": one kernel), or from torch's generator in the eager learner's order (rng="torch": the slots
+        via ring.sample_indices, then N(0, scale) [B, 4]), or (tests) from idx / noise: the slots and the UNCLIPPED
+        N(0, scale) noise."""
         L, st, b = self.L, self._stream(), self.buf
-        i = self.ring.sample_indices(self.B) if idx is None else idx
-        self.idx.copy_(i)
+        c = self.cfg
+        prioritized = self.ring.prioritized
+        if idx is None and noise is None and self.rng == "device" and not prioritized:
+            _check(L.hkl_sample(ctypes.byref(self.sio), st), "hkl_sample")
+            i = self.idx
+        else:
+            i = self.ring.sample_indices(self.B) if idx is None else idx
+            self.idx.copy_(i)
+            if noise is None:
+                noise = torch.randn((self.B, 4), device=self.agent.device) * c.target_action_noise_scale
+            b["noise"].copy_(torch.clamp(noise, -c.target_action_noise_clip, c.target_action_noise_clip))
         if self.iw is not None:
             wb = self.ring.w[i]
             p = wb / wb.sum()
             iw = (1.0 / (p * self.ring.size_t)) ** self.ring.beta
             self.iw.copy_(iw / iw.max())
-        c = self.cfg
-        if noise is None:
-            noise = torch.randn((self.B, 4), device=self.agent.device) * c.target_action_noise_scale
-        b["noise"].copy_(torch.clamp(noise, -c.target_action_noise_clip, c.target_action_noise_clip))
         _check(L.hkl_critic_step(ctypes.byref(self.cio), st), "hkl_critic_step")
         _check(L.hkl_wgrad(self.wg["c256"], 2, 256, self.B, st), "hkl_wgrad")
         _check(L.hkl_wgrad(self.wg["c32"], 2, XP, self.B, st), "hkl_wgrad")

@@ -400,9 +400,10 @@ class Learner:
     fused: True runs every update through the fused fp32 MFMA kernels (hockey_amd.learner_hip: a handful of HIP
     kernels per update; batches that are multiples of 256, GPU only, fails loudly without the library); False
     through PyTorch ops; "auto" (default) picks fused for GPU batches of at least FUSED_MIN_BATCH when the library is
-    built."""
+    built.  fused_rng: "device" (the batch's slots and target noise from the fused learner's Philox stream, one
+    kernel) or "torch" (torch's generator, in the eager learner's order)."""
 
-    def __init__(self, agent, ring, batch, graphs=True, warm_pairs=3, fused="auto"):
+    def __init__(self, agent, ring, batch, graphs=True, warm_pairs=3, fused="auto", fused_rng="device"):
         self.agent, self.ring, self.batch = agent, ring, int(batch)
         self.use_graph = bool(graphs) and agent.device.type == "cuda" and agent.cfg.policy_update_freq == 2
         self.warm_left = int(warm_pairs)
@@ -414,7 +415,7 @@ class Learner:
         self.fused = None
         if fused:
             from .learner_hip import FusedLearner
-            self.fused = FusedLearner(agent, ring, self.batch)
+            self.fused = FusedLearner(agent, ring, self.batch, rng=fused_rng)
             self.fused.set_loss_accumulator(self.acc)
 
     def _one(self, train_actor=None):

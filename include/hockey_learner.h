@@ -46,6 +46,7 @@ typedef struct {
   float *x0, *h1[2], *dz1[2], *dz2[2];
   float *p_db1[2], *p_db2[2], *p_dw3[2], *p_db3[2];
   float *p_loss, *td;
+  int64_t *sample_counter; /* optional: hkl_sample's update counter, advanced by one at the end */
 } hkl_critic_io;
 
 /* update_actor forward / backward: actor(s), Q1(s, actor(s)) of the updated critic, d(-mean Q1).  Outputs: X0
@@ -94,7 +95,8 @@ int hkl_pack_floats(void);
 int hkl_pack(const hkl_net *nets, int n_nets, int64_t *step, void *stream);
 int hkl_critic_step(const hkl_critic_io *io, void *stream);
 int hkl_actor_step(const hkl_actor_io *io, void *stream);
-/* weight-gradient job: slab[c][256][k_width] = sum over the samples j of chunk c (256 each) of dz[j][o] x[j][k]
+/* weight-gradient job: slab[c][256][k_width] = sum over the samples j of chunk c (k_width 256: 512 samples each
+ * when the batch is a multiple of 512, else 256; k_width 32: 256) of dz[j][o] x[j][k]
  * (dz [B][256], x [B][k_width]); bias_slab (optional) [c][256] = the chunk's column sums of dz */
 typedef struct {
   const float *dz, *x;
@@ -105,6 +107,18 @@ int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch,
 int hkl_adam(const hkl_adam_io *io, void *stream);
 /* target = target * rho + tau * param over n floats (soft_update; tau = 1 - rho) */
 int hkl_polyak(float *target, const float *param, int64_t n, float rho, float tau, void *stream);
+
+/* the batch's replay slots idx[B] (uniform over the ring's *size filled slots) and clipped target noise [B][4]
+ * from Philox4x32-10 keyed by seed, counter = *counter (device; hkl_critic_step advances it) */
+typedef struct {
+  int64_t batch;
+  uint64_t seed;
+  const int64_t *counter, *size;
+  int64_t *idx;
+  float *noise;
+  float scale, clip;
+} hkl_sample_io;
+int hkl_sample(const hkl_sample_io *io, void *stream);
 
 /* y = the kernels' tanh of x (n floats; a test probe of the activation's accuracy) */
 int hkl_tanh_probe(const float *x, float *y, int64_t n, void *stream);

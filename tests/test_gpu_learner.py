@@ -108,7 +108,7 @@ def test_fused_learner_matches_reference_learner_g9b():
 
 def test_fused_learner_matches_eager_learner_on_ring():
     """Fused vs eager (PyTorch) learner from the same weights and ring, with the same torch RNG stream (slots, then
-    target noise): 8 updates of 4096 samples."""
+    target noise; the fused learner's torch-RNG mode): 8 updates of 4096 samples."""
     cfg = TD3Config()
     torch.manual_seed(7)
     cap = 50_000
@@ -119,7 +119,7 @@ def test_fused_learner_matches_eager_learner_on_ring():
     ring_e.push(s, a, r, s2, d)
     eager, fused = TD3(cfg, device=DEV, seed=3), TD3(cfg, device=DEV, seed=3)
     le = Learner(eager, ring_e, 4096, graphs=False, fused=False)
-    lf = Learner(fused, ring_e, 4096, graphs=False, fused=True)
+    lf = Learner(fused, ring_e, 4096, graphs=False, fused=True, fused_rng="torch")
     for k in range(8):
         torch.manual_seed(100 + k)
         le._one()
@@ -168,3 +168,34 @@ def test_fused_tanh_accuracy():
     x = torch.cat([torch.linspace(-20, 20, 1_000_001, device=DEV), torch.linspace(-1e-3, 1e-3, 100_001, device=DEV)])
     err = (tanh_probe(x).double() - torch.tanh(x.double())).abs().max().item()
     assert err < 2e-7, err
+
+
+def test_device_sampling_distribution():
+    """The fused learner's device sampling (rng="device"): slots uniform over the filled ring (odd / even and halves
+    balanced at a fill level past 2^24) and target noise with the N(0, 0.2) moments, clipped to +-0.3."""
+    from hockey_amd.learner_hip import FusedLearner
+
+    cfg = TD3Config()
+    agent = TD3(cfg, device=DEV, seed=1)
+    ring = ReplayRing(1024, device=DEV)
+    ring.push(torch.zeros(1024, 18, device=DEV), torch.zeros(1024, 4, device=DEV), torch.zeros(1024, device=DEV),
+              torch.zeros(1024, 18, device=DEV), torch.zeros(1024, device=DEV))
+    fl = FusedLearner(agent, ring, 16384)
+    size = 2 ** 25 + 3
+    ring.size_t.fill_(size)  # sampling reads only the fill level
+    idx, noise = [], []
+    for _ in range(16):
+        fl.L.hkl_sample(__import__("ctypes").byref(fl.sio), fl._stream())
+        fl.sample_counter += 1
+        idx.append(fl.idx.clone())
+        noise.append(fl.buf["noise"].clone())
+    i, z = torch.cat(idx), torch.cat(noise)
+    assert int(i.min()) >= 0 and int(i.max()) < size
+    assert abs(float((i % 2 == 1).double().mean()) - 0.5) < 0.01
+    assert abs(float((i >= size // 2).double().mean()) - 0.5) < 0.01
+    assert len(torch.unique(idx[0])) > 16000  # consecutive counters give different batches
+    assert float(z.abs().max()) <= 0.3 + 1e-7
+    inner = z[z.abs() < 0.29]
+    assert abs(float(inner.mean())) < 0.003
+    clip_share = float((z.abs() >= 0.3 - 1e-7).double().mean())
+    assert abs(clip_share - 0.1336) < 0.01, clip_share  # P(|N(0, 0.2)| > 0.3) = 2 (1 - Phi(1.5))
