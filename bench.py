@@ -44,6 +44,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # fp32 VALU lane-operation peak: 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: 157.3 TFLOPS
 # counts an FMA as 2).  One wave per SIMD (this kernel's occupancy) issues a VALU op every 4 cycles, not 2.
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md), an FMA counted as 2
 
 
 def _args():
@@ -522,6 +523,13 @@ def main():
         lib_hash, src_hash = provenance()
         stale = (sq.get("source_hash") != lib_hash or pmc.get("source_hash") != lib_hash or lib_hash != src_hash)
         lane_ops = sq.get("valu_lane_ops_per_launch")
+        flops = None
+        try:  # algorithmic FLOPs per env-step of this workload (scripts/flop_count.py, host build of the kernel source)
+            with open(os.path.join(ROOT, "profiles", "r04", "flop_count.json")) as f:
+                flops = json.load(f)["flops_per_env_step"] if args.policy == "basic" else None
+        except Exception:  # noqa: BLE001
+            flops = None
+        useful_tflops = flops * n / (kern_ms * 1e-3) / 1e12 if flops else None
         valu_tops = lane_ops / (kern_ms * 1e-3) / 1e12 if lane_ops else None
         line = {
             "metric": "env-steps/sec at 65536 arenas per MI355X (BASELINE.json metric)",
@@ -542,6 +550,10 @@ def main():
                        "parallelism": f"arena-sharded x{world} (no collectives)"},
             "roofline": {"bound": "valu", "achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
                          "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
+                         "useful_frac": useful_tflops / FP32_PEAK_TFLOPS if useful_tflops else None,
+                         "useful": {"flops_per_env_step": flops, "achieved": useful_tflops, "peak": FP32_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "from": "profiles/r04/flop_count.json (algorithmic FLOPs of "
+                                                              "Box2D's arithmetic, scripts/flop_count.py)"},
                          "traffic": pmc.get("hbm_bytes_per_launch"),
                          "kernel": "hk::step_kernel", "kernel_avg_ms": kern_ms,
                          "valu_lane_ops_per_launch": lane_ops,

@@ -124,8 +124,22 @@ HK_DEV float fmax2(float a, float b) { return a > b ? a : b; }
 HK_DEV float fclamp(float a, float lo, float hi) { return fmax2(lo, fmin2(a, hi)); }
 HK_DEV float fabs2(float a) { return a > 0.0f ? a : -a; }
 
+// Host harness only (hostcheck, HK_HOST_DIAG): event counts behind the algorithmic FLOP count of an env-step
+// (scripts/flop_count.py multiplies them by the FLOPs each event's source performs).  No-op in the product build.
+enum {
+  EV_VEL1 = 0, EV_VEL2, EV_POS_PT, EV_INIT, EV_INIT_PT, EV_INIT_BLOCK, EV_WARM_PT, EV_POLY_CIRCLE, EV_POLYGONS,
+  EV_GJK, EV_GJK_IT, EV_ROT, EV_TOI, EV_SEP_MIN, EV_SEP_EVAL, EV_STEP, EV_N
+};
+#ifdef HK_HOST_DIAG
+extern unsigned long long g_hk_flop_ev[EV_N];
+#define HK_EV(k, n) (g_hk_flop_ev[k] += (unsigned long long)(n))
+#else
+#define HK_EV(k, n) ((void)0)
+#endif
+
 // deterministic sin/cos for b2Rot::Set (bit-identical to the oracle's hk_sincosf)
 HK_DEV rot rot_set(float x) {
+  HK_EV(EV_ROT, 1);
   float fj = rintf(x * 0.636619772367581343f);
   int j = (int)fj;
   float r = ((x - fj * 1.5703125f) - fj * 4.837512969970703125e-4f) - fj * 7.549789954891882e-8f;

@@ -69,6 +69,7 @@ HK_DEV v2 fxn(const RFix<N> &f, int i) {
 // b2CollidePolygonAndCircle (the circle's centre is its local position cb.vx[0], cb.vy[0])
 template <int NA>
 HK_DEV void collide_poly_circle(Manifold &m, const RFix<NA> &pa, xform xfA, const RFix<1> &cb, xform xfB) {
+  HK_EV(EV_POLY_CIRCLE, 1);
   m.count = 0;
   const v2 cpos = V(cb.vx[0], cb.vy[0]);
   v2 c = mul_xv(xfB, cpos);
@@ -229,6 +230,7 @@ HK_DEV void clip_polygons(Manifold &m, const RFix<N1> &p1, xform xf1, int edge1,
 // b2CollidePolygons
 template <int NA, int NB>
 HK_DEV void collide_polygons(Manifold &m, const RFix<NA> &pA, xform xfA, const RFix<NB> &pB, xform xfB) {
+  HK_EV(EV_POLYGONS, 1);
   m.count = 0;
   float total = pA.radius + pB.radius;
   int eA = 0, eB = 0;
@@ -408,10 +410,12 @@ HK_DEV void solve3(Simplex &s) {
 template <typename PA, typename PB>
 HK_DEV float gjk_distance(SimplexCache &cache, const PA &pA, xform xA, const PB &pB, xform xB, int use_radii) {
   Simplex s;
+  HK_EV(EV_GJK, 1);
   simplex_read(s, cache, pA, xA, pB, xB);
   int sA0 = 0, sA1 = 0, sA2 = 0, sB0 = 0, sB1 = 0, sB2 = 0, saveCount;
   int iter = 0;
   while (iter < 20) {
+    HK_EV(EV_GJK_IT, 1);
     saveCount = s.count;
     sA0 = s.v1.iA; sB0 = s.v1.iB;
     sA1 = s.v2.iA; sB1 = s.v2.iB;
@@ -541,6 +545,7 @@ HK_DEV void sep_init(SepFn<PA, PB> &f, const SimplexCache &cache, const PA &pA, 
 }
 template <typename PA, typename PB>
 HK_DEV float sep_find_min(const SepFn<PA, PB> &f, int &iA, int &iB, float t) {
+  HK_EV(EV_SEP_MIN, 1);
   xform xA, xB;
   sweep_xf_of<PA>(f.sA, xA, t);
   sweep_xf_of<PB>(f.sB, xB, t);
@@ -570,6 +575,7 @@ HK_DEV float sep_find_min(const SepFn<PA, PB> &f, int &iA, int &iB, float t) {
 }
 template <typename PA, typename PB>
 HK_DEV float sep_eval(const SepFn<PA, PB> &f, int iA, int iB, float t) {
+  HK_EV(EV_SEP_EVAL, 1);
   xform xA, xB;
   sweep_xf_of<PA>(f.sA, xA, t);
   sweep_xf_of<PB>(f.sB, xB, t);
@@ -593,6 +599,7 @@ enum { TOI_UNKNOWN = 0, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED 
 
 template <typename PA, typename PB>
 HK_DEV int time_of_impact(const PA &pA, const PB &pB, Sweep sA, Sweep sB, float tMax, float &t_out) {
+  HK_EV(EV_TOI, 1);
   int state = TOI_UNKNOWN;
   t_out = tMax;
   sweep_normalize(sA);

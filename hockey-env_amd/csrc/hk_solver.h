@@ -189,6 +189,9 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
   s.ny = normal.y;
   const float re = SLDS.restitution[p];
   const int vcount = fs_vcount(s);
+  HK_EV(EV_INIT, 1);
+  HK_EV(EV_INIT_PT, vcount);
+  HK_EV(EV_INIT_BLOCK, vcount == 2);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (j < vcount) {
@@ -230,6 +233,7 @@ HK_DEV void fslot_init_velocity(FSlot &s, const Arena &w) {
 
 HK_DEV void fslot_warm_start(const FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s), vcount = fs_vcount(s);
+  HK_EV(EV_WARM_PT, vcount);
   v2 vA, vB;
   float wA, wB;
   get_vel_a(B, bA, vA, wA);
@@ -268,6 +272,7 @@ template <bool kSA = false, int kP = 0>
 HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &wB) {
   const float mA = s.mA, iA = s.iA, mB = s.mB, iB = s.iB;
   const int vcount = kP ? kP : fs_vcount(s);
+  HK_EV(vcount == 1 ? EV_VEL1 : EV_VEL2, 1);
   const f2 normal = f2{s.nx, s.ny}, tangent = f2{1.0f * s.ny, -1.0f * s.nx};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -371,6 +376,7 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
   Dyn &B = w.d;
   const float mA = s.mA, mB = s.mB, iA = s.iA, iB = s.iB;
   const int bA = fs_bA(s), bB = fs_bB(s), pcount = fs_pcount(s);
+  HK_EV(EV_POS_PT, pcount);
   const f2 lcA = F2(local_center(bA)), lcB = F2(local_center(bB));
   const float rAr = pair_rA(), rBr = pair_rB(bB);
   v2 cA0, cB0;

@@ -287,6 +287,7 @@ struct LaneOut { int done_edge, win1, win2, ntoi, ovf, nbig, bad_policy; };
 // m: the step's HBM words (fetch_words), fetched by the caller so that it can issue them early
 HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int64_t a, float *lds, int lane,
                       PhaseT &T, LaneOut &out, const StepWords &m) {
+  HK_EV(EV_STEP, 1);
   Arena w;
   unpack_arena(w, m.f, m.i, a, s, cfg.keep_mode, cfg.vel_ref, lds, lane);
   w.force_big = cfg.diag & 1;

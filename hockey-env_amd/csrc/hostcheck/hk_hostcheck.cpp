@@ -41,6 +41,7 @@ constexpr hk::Scene g_scene =  // the kernels' compile-time scene (hk_scene_gen.
 #include "../hk_step.h"
 
 unsigned long long hk::g_hk_host_diag[4];
+unsigned long long hk::g_hk_flop_ev[hk::EV_N];
 
 using namespace hk;
 
@@ -139,6 +140,13 @@ void hkh_raw(void *h, float **f, int32_t **i) {
   *f = c->f.data();
   *i = c->i.data();
 }
+
+// event counts of the algorithmic FLOP count (hk_core.h HK_EV), process-wide; read and cleared
+void hkh_flop_events(unsigned long long *out) {
+  std::memcpy(out, hk::g_hk_flop_ev, sizeof(hk::g_hk_flop_ev));
+  std::memset(hk::g_hk_flop_ev, 0, sizeof(hk::g_hk_flop_ev));
+}
+int hkh_flop_event_count(void) { return hk::EV_N; }
 
 // velocity-loop coverage counters (hk_solver.h HK_HOST_DIAG_INC), process-wide; read and cleared
 void hkh_diag(unsigned long long *out4) {
