@@ -132,3 +132,50 @@ def test_facade_phase_increment_is_the_reference_draw():
     np.random.seed(1234)
     got = [0.2 * np.random.random() for _ in range(20000)]
     assert np.array(got).view(np.uint64).tolist() == np.array(want).view(np.uint64).tolist()
+
+
+def _declared_learner():
+    src = open(os.path.join(ROOT, "include", "hockey_learner.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hkl_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_learner_library_exports_every_declared_symbol():
+    """libhockey_learner.so (the fused TD3 learner, include/hockey_learner.h) loads without a GPU and exports every
+    declared entry point; the ctypes binding lists the same set."""
+    from hockey_amd import learner_hip as LH
+
+    if not os.path.exists(LH.LIB_PATH):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "hockey-env_amd", "csrc"), "learner"])
+    L = ctypes.CDLL(LH.LIB_PATH)
+    missing = [n for n in _declared_learner() if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(_declared_learner()) == set(LH.EXPORTS)
+    assert LH.lib().hkl_pack_floats() == LH.PACK_FLOATS
+
+
+def test_learner_ctypes_struct_layout_matches_header(tmp_path):
+    """Sizes and field offsets of the learner's ABI structs as the C compiler lays them out from the header."""
+    import subprocess
+
+    from hockey_amd import learner_hip as LH
+
+    probes = {"Net": "hkl_net", "CriticIO": "hkl_critic_io", "ActorIO": "hkl_actor_io", "Seg": "hkl_seg",
+              "AdamIO": "hkl_adam_io", "WgJob": "hkl_wgrad_job", "SampleIO": "hkl_sample_io"}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hockey_learner.h"', "int main(void) {"]
+    for py, cname in probes.items():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in getattr(LH, py)._fields_:
+            lines.append(f'  printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    want = dict(line.split() for line in subprocess.check_output([str(exe)], text=True).splitlines())
+    for py, cname in probes.items():
+        S = getattr(LH, py)
+        assert ctypes.sizeof(S) == int(want[cname]), cname
+        for f, _ in S._fields_:
+            assert getattr(S, f).offset == int(want[f"{cname}.{f}"]), (cname, f)
