@@ -75,12 +75,18 @@ struct Net {  // device view of one MLP (n_in -> 256 -> 256 -> n_out)
 __host__ __device__ inline Net net_of(const hkl_net &n) { return Net{n.w1, n.b1, n.w2, n.b2, n.w3, n.b3, n.pack, n.n_in, n.n_out}; }
 
 // ------------------------------------------------------------------------------------------------ layer routines
-// out = W1 x (no bias): x[s] = this lane's input for k-step s (feature 4 s + (lane >> 4))
-__device__ __forceinline__ void gemm_in(const float *__restrict__ f1, const float (&x)[S1], Tile &out, int lane) {
+// out = W1 x (no bias): x[s] = this lane's input for k-step s (feature 4 s + (lane >> 4)).  Workgroup-collective:
+// the 32 KB first-layer pack is staged in LDS (both fragment buffers) once for the 4 waves.
+__device__ __forceinline__ void gemm_in(const float *__restrict__ f1, const float (&x)[S1], Tile &out, int lane,
+                                        f4 *sfrag) {
+  const f4 *src = reinterpret_cast<const f4 *>(f1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sfrag[threadIdx.x + i * WG] = src[threadIdx.x + i * WG];
+  __syncthreads();
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) {
-    const f4 lo = *reinterpret_cast<const f4 *>(f1 + (ob * 64 + lane) * 8);
-    const f4 hi = *reinterpret_cast<const f4 *>(f1 + (ob * 64 + lane) * 8 + 4);
+    const f4 lo = sfrag[(ob * 64 + lane) * 2];
+    const f4 hi = sfrag[(ob * 64 + lane) * 2 + 1];
     f4 acc = z4();
     acc = mfma(lo[0], x[0], acc);
     acc = mfma(lo[1], x[1], acc);
@@ -90,6 +96,7 @@ __device__ __forceinline__ void gemm_in(const float *__restrict__ f1, const floa
     acc = mfma(hi[1], x[5], acc);
     out.v[ob] = acc;
   }
+  __syncthreads();  // the staging buffers are reused by the next collective call
 }
 
 // out = P in, P a packed 256 x 256 operand (fp: W2 in; bp: W2^T in), a workgroup-collective call (all 4 waves).
@@ -277,7 +284,7 @@ __device__ __forceinline__ void input_frags(const float *__restrict__ srow, cons
 // Q(x) of one critic network (forward only): its output for this lane's sample
 __device__ __forceinline__ float q_forward(const Net &c, const float (&x)[S1], Tile &h1, Tile &h2, int lane,
                                            f4 *sfrag) {
-  gemm_in(c.f1(), x, h1, lane);
+  gemm_in(c.f1(), x, h1, lane, sfrag);
   gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
   return gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane, sfrag)[0];
 }
@@ -289,7 +296,7 @@ __device__ __forceinline__ void critic_one(const hkl_critic_io &io, int k, const
                                            float w, int64_t row, float *red, f4 *sfrag, float &td, float &loss) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4;
   Tile h1, h2;
-  gemm_in(c.f1(), x, h1, lane);
+  gemm_in(c.f1(), x, h1, lane, sfrag);
   gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
   store_tile(io.h1[k], h1, row, q);
   const float qv = gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane, sfrag)[0];
@@ -333,7 +340,7 @@ __global__ void __launch_bounds__(WG, 1) critic_step_kernel(hkl_critic_io io) {
   float x[S1];
   input_frags(s2_row, z4(), false, x, q);
   Tile h1, h2;
-  gemm_in(ta.f1(), x, h1, lane);
+  gemm_in(ta.f1(), x, h1, lane, sfrag);
   gemm256(ta.fp(), h1, ta.b1, h2, lane, sfrag);
   const f4 a2 = gemm_out(ta.fo(), h2, ta.b2, ta.b3, 4, lane, sfrag);
   f4 a2u;
@@ -389,7 +396,7 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
     }
   }
   Tile h1, h2;
-  gemm_in(an.f1(), x, h1, lane);
+  gemm_in(an.f1(), x, h1, lane, sfrag);
   gemm256(an.fp(), h1, an.b1, h2, lane, sfrag);
   store_tile(io.h1, h1, row, q);
   const f4 pre = gemm_out(an.fo(), h2, an.b2, an.b3, 4, lane, sfrag);
@@ -402,7 +409,7 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   }
   // Q1(s, a)
   input_frags(s_row, au, true, x, q);
-  gemm_in(qn.f1(), x, h1, lane);
+  gemm_in(qn.f1(), x, h1, lane, sfrag);
   gemm256(qn.fp(), h1, qn.b1, h2, lane, sfrag);
   const float qv = gemm_out(qn.fo(), h2, qn.b2, qn.b3, 1, lane, sfrag)[0];
   const float g = -1.0f / (float)io.batch;  // d(-mean q) / dq

@@ -111,6 +111,10 @@ class HockeyEnv:
         self._step_flags = 0  # HK_STEP_* (the golden harness sets HK_STEP_SKIP_PHYSICS)
         self._host_ptrs = (self._act_np.ctypes.data_as(ctypes.c_void_p), self._inc_np.ctypes.data_as(ctypes.c_void_p),
                            self._out_np.ctypes.data_as(ctypes.c_void_p))
+        # the step's fixed call arguments: context, flags are read per call; the stream is the one current at
+        # construction (a facade is a single-stream object, like the reference env)
+        self._step_fn = self._vec.L.hk_step_host
+        self._step_stream = self._vec._stream()
         self._ptr = {k: ctypes.c_void_p(base + off) for k, off in
                      (("obs", _OBS), ("obs2", _OBS2), ("info", _INFO), ("info2", _INFO2), ("reward", _REW),
                       ("reward2", _REW2), ("aux", _AUXI))}
@@ -145,7 +149,9 @@ class HockeyEnv:
         set_state the obs, info / rewards and aux of the current state are computed on the device and copied to
         the host in one transfer."""
         if stepped:
-            self._snap = _Snap(self._out_obs.astype(np.float64), self._out_obs2.copy(), self._out_f.copy())
+            # obs2 / f stay views of the step's out buffer: the snapshot is replaced by the next step, which is the
+            # only writer of that buffer
+            self._snap = _Snap(self._out_obs.astype(np.float64), self._out_obs2, self._out_f)
             return self._snap
         L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
         p = self._ptr
@@ -192,11 +198,15 @@ class HockeyEnv:
             inc_p = None
         elif opp_inc is not True:
             self._inc_np[:] = opp_inc
-        N.check(self._vec.L.hk_step_host(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._vec._stream()),
-                "hk_step_host")
+        rc = self._step_fn(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._step_stream)
+        if rc:
+            N.check(rc, "hk_step_host")
         s = self._refresh(stepped=True)
         f = s.f
-        return self._obs_out(s.obs), float(f[8]), bool(f[13]), False, self._info_dict(f[0:4])
+        obs = s.obs if self.keep_mode else s.obs[:16].copy()  # a fresh float64 array either way
+        return obs, float(f[8]), bool(f[13]), False, {"winner": int(f[0]), "reward_closeness_to_puck": float(f[1]),
+                                                      "reward_touch_puck": float(f[2]),
+                                                      "reward_puck_direction": float(f[3])}
 
     def step(self, action):
         a = np.clip(np.asarray(action, np.float64), -1, +1).astype(np.float32)  # hockey_env.py:659
