@@ -10,4 +10,6 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 
 rc=$?; tail -15 $O/pytest_learner.log; [ $rc -eq 0 ] || { grep -B2 -A30 "Error\|assert" $O/pytest_learner.log | head -80; exit $rc; }
 timeout -k 10 300 python -u scripts/learner_profile.py 16384 100 > $O/learner_profile.log 2>&1 || { tail -20 $O/learner_profile.log; exit 1; }
 tail -1 $O/learner_profile.log
+timeout -k 10 300 python -u scripts/learner_profile.py 256 400 > $O/learner_profile_b256.log 2>&1 || { tail -20 $O/learner_profile_b256.log; exit 1; }
+tail -1 $O/learner_profile_b256.log
 bash scripts/gpu_r04d.sh
