@@ -380,7 +380,9 @@ class TD3:
                 "target_critic": sd(self.target_critic)}
 
 
-FUSED_MIN_BATCH = 4096  # fused="auto": the MFMA learner from this batch up (C5 draws 16 384 per update)
+FUSED_MIN_BATCH = 256  # fused="auto": the MFMA learner for batches of 256 and up (its chunk granularity): 0.32 ms
+# per update at the reference's batch 256 against 1.44 ms for the graph-captured PyTorch pair, 0.39 ms at C5's 16 384
+# (profiles/r04/learner_profile*.log)
 
 
 def fused_available():
@@ -399,9 +401,9 @@ class Learner:
 
     fused: True runs every update through the fused fp32 MFMA kernels (hockey_amd.learner_hip: a handful of HIP
     kernels per update; batches that are multiples of 256, GPU only, fails loudly without the library); False
-    through PyTorch ops; "auto" (default) picks fused for GPU batches of at least FUSED_MIN_BATCH when the library is
-    built.  fused_rng: "device" (the batch's slots and target noise from the fused learner's Philox stream, one
-    kernel) or "torch" (torch's generator, in the eager learner's order)."""
+    through PyTorch ops; "auto" (default) picks fused for GPU batches of at least FUSED_MIN_BATCH (multiples of 256)
+    at hidden width 256 when the library is built.  fused_rng: "device" (the batch's slots and target noise from the
+    fused learner's Philox stream, one kernel) or "torch" (torch's generator, in the eager learner's order)."""
 
     def __init__(self, agent, ring, batch, graphs=True, warm_pairs=3, fused="auto", fused_rng="device"):
         self.agent, self.ring, self.batch = agent, ring, int(batch)
@@ -411,7 +413,7 @@ class Learner:
         self.acc = torch.zeros(4, dtype=torch.float64, device=agent.device)  # sum critic, sum actor, n c, n a
         if fused == "auto":
             fused = (agent.device.type == "cuda" and self.batch >= FUSED_MIN_BATCH and self.batch % 256 == 0 and
-                     fused_available())
+                     agent.actor.fc1.out_features == 256 and fused_available())
         self.fused = None
         if fused:
             from .learner_hip import FusedLearner
