@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,8 +44,21 @@ struct Ctx {
   // variant instead (device buffer hs_dev, one H2D and one D2H copy per step) for A/B timing.
   uint8_t *hs_pin = nullptr, *hs_map = nullptr, *hs_dev = nullptr;
   int hs_staged = 0;
-  uint64_t hs_seq = 0;  // hk_step_host launches so far (the completion word's expected value)
+  uint64_t hs_seq = 0;  // hk_step_host steps so far (the completion word's expected value)
+  // hk_step_host's resident server (mapped variant; HK_STEP_HOST_SERVER=0 launches one step kernel per call
+  // instead): it runs on a private stream, ordered after the caller's stream when it starts, and every other
+  // entry point stops it first (server_stop), so it never runs beside another kernel of this context.
+  int srv_on = 0;
+  hipStream_t srv_stream = nullptr;
+  hipEvent_t srv_after = nullptr;
+  bool srv_running = false;
+  std::chrono::steady_clock::time_point srv_start, srv_last;
+  unsigned long long srv_idle_ticks = 0, srv_life_ticks = 0;
 };
+
+// the server's own limits (hk_kernels.h HostServer): it exits after kSrvIdleMs without a request or kSrvLifeMs in
+// all; the host replaces it before either can fire mid-request (half those times), and relaunches on demand
+constexpr int kSrvIdleMs = 20, kSrvLifeMs = 2000;
 
 // hk_step_host buffer layout per context: inputs [N,8] f32 actions + [N,2] f64 increments, outputs [N] packed
 // records of HK_HOST_RECORD_BYTES (obs f32[18], obs2 f32[18], done u8 + 7 pad, record f64[16])
@@ -52,8 +66,31 @@ constexpr size_t kHostObs = 0, kHostObs2 = 72, kHostDone = 144, kHostRec = 152;
 static_assert(kHostRec + 16 * 8 == HK_HOST_RECORD_BYTES, "hk_step_host record layout");
 size_t host_in_bytes(int64_t n) { return (size_t)n * (8 * 4 + 2 * 8); }
 constexpr size_t kHostWordBytes = 64;  // the completion word (hk_step_host), on its own 64-B line
-// offset of the completion word in the pinned buffer: the inputs and the records, rounded up to a 64-B line
+// offset of the completion word in the pinned buffer: the inputs and the records, rounded up to a 64-B line; the
+// server's request word and its argument words follow on lines of their own
 size_t host_word_off(int64_t n) { return (host_in_bytes(n) + (size_t)n * HK_HOST_RECORD_BYTES + 63) & ~(size_t)63; }
+size_t host_req_off(int64_t n) { return host_word_off(n) + kHostWordBytes; }
+size_t host_args_off(int64_t n) { return host_word_off(n) + 2 * kHostWordBytes; }
+size_t host_pin_bytes(int64_t n) { return host_word_off(n) + 3 * kHostWordBytes; }
+
+volatile uint64_t *req_word(Ctx *c) { return reinterpret_cast<volatile uint64_t *>(c->hs_pin + host_req_off(c->s.n)); }
+
+// stop hk_step_host's server (if one runs) and wait for it: every request it was given has been answered (a step
+// returns only then), so the next server starts idle
+hipError_t server_stop(Ctx *c) {
+  if (!c->srv_running) return hipSuccess;
+  std::atomic_thread_fence(std::memory_order_release);
+  *req_word(c) = hk::kServerQuit;
+  const hipError_t e = hipStreamSynchronize(c->srv_stream);
+  *req_word(c) = c->hs_seq;
+  c->srv_running = false;
+  return e;
+}
+#define HK_QUIESCE(c, who)                                               \
+  do {                                                                   \
+    const hipError_t qe_ = server_stop(c);                               \
+    if (qe_ != hipSuccess) return hipfail(qe_, who ": step server");     \
+  } while (0)
 
 
 int check_policy(int p) { return p >= HK_POLICY_EXTERNAL && p <= HK_POLICY_BASIC_STRONG; }
@@ -139,6 +176,9 @@ int hk_destroy(void *ctx) {
   if (!ctx) return HK_OK;
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  (void)server_stop(c);
+  if (c->srv_stream) (void)hipStreamDestroy(c->srv_stream);
+  if (c->srv_after) (void)hipEventDestroy(c->srv_after);
   if (c->s.f) (void)hipFree(c->s.f);
   if (c->s.i) (void)hipFree(c->s.i);
   if (c->s.man) (void)hipFree(c->s.man);
@@ -156,7 +196,10 @@ int64_t hk_num_arenas(const void *ctx) { return ctx ? ((const Ctx *)ctx)->s.n : 
 int hk_set_policy(void *ctx, int player, int policy) {
   if (!ctx) return fail(HK_E_INVALID, "hk_set_policy: ctx is NULL%s");
   if (player < 0 || player > 1 || !check_policy(policy)) return fail(HK_E_INVALID, "hk_set_policy: bad args%s");
-  ((Ctx *)ctx)->cfg.policy[player] = policy;
+  Ctx *c = (Ctx *)ctx;
+  DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_set_policy");  // a running server holds the old configuration
+  c->cfg.policy[player] = policy;
   return HK_OK;
 }
 
@@ -165,6 +208,7 @@ int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t 
   if (!ctx) return fail(HK_E_INVALID, "hk_reset: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_reset");
   hipError_t e = hk::launch_reset(c->s, c->cfg, mask, params, max_t, one_starts, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_reset");
 }
@@ -194,6 +238,10 @@ static int launch_steps(const char *who, void *ctx, const hk_step_io *io, int ns
   s.policy2 = io->policy2;
   s.record = io->record;
   DeviceGuard g(c->device);
+  {
+    const hipError_t qe = server_stop(c);
+    if (qe != hipSuccess) return hipfail(qe, who);
+  }
   hipError_t e = hk::launch_step(c->s, c->cfg, s, nsteps, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, who);
 }
@@ -213,9 +261,11 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
   if (!c->hs_pin) {
     const char *v = std::getenv("HK_STEP_HOST_STAGED");
     c->hs_staged = v && v[0] == '1';
+    const char *sv = std::getenv("HK_STEP_HOST_SERVER");
+    c->srv_on = !c->hs_staged && !(sv && sv[0] == '0');
     if (c->hs_staged && (e = hipMalloc(&c->hs_dev, in_b + out_b)) != hipSuccess)
       return hipfail(e, "hk_step_host: hipMalloc");
-    const size_t pin_b = host_word_off(n) + kHostWordBytes;
+    const size_t pin_b = host_pin_bytes(n);
     if ((e = hipHostMalloc(&c->hs_pin, pin_b, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&c->hs_map, c->hs_pin, 0)) != hipSuccess) {
       if (c->hs_pin) (void)hipHostFree(c->hs_pin);
@@ -227,9 +277,84 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
     // expected sequence number (1) would end the first wait before the kernel ran
     std::memset(c->hs_pin, 0, pin_b);
     c->hs_seq = 0;
+    if (c->srv_on) {
+      int khz = 0;
+      if ((e = hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&c->srv_after, hipEventDisableTiming)) != hipSuccess ||
+          (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device)) != hipSuccess)
+        return hipfail(e, "hk_step_host: server stream");
+      c->srv_idle_ticks = (unsigned long long)khz * kSrvIdleMs;
+      c->srv_life_ticks = (unsigned long long)khz * kSrvLifeMs;
+    }
   }
   const hipStream_t st = (hipStream_t)stream;
   const size_t a_b = (size_t)n * 8 * 4, inc_b = (size_t)n * 2 * 8;
+  if (c->srv_on) {
+    // A server that has idled or lived for half its limits may be about to exit on its own: replace it now
+    // rather than post a request it could miss (a missed request is still served: see the wait below).
+    const auto now = std::chrono::steady_clock::now();
+    if (c->srv_running && (now - c->srv_last > std::chrono::milliseconds(kSrvIdleMs / 2) ||
+                           now - c->srv_start > std::chrono::milliseconds(kSrvLifeMs / 2))) {
+      if ((e = server_stop(c)) != hipSuccess) return hipfail(e, "hk_step_host: step server");
+    }
+    if (actions) std::memcpy(c->hs_pin, actions, a_b);
+    if (opp_inc) std::memcpy(c->hs_pin + a_b, opp_inc, inc_b);
+    volatile int32_t *args = reinterpret_cast<volatile int32_t *>(c->hs_pin + host_args_off(n));
+    args[0] = flags;
+    args[1] = actions ? 1 : 0;
+    args[2] = opp_inc ? 1 : 0;
+    const uint64_t seq = ++c->hs_seq;
+    std::atomic_thread_fence(std::memory_order_release);
+    *req_word(c) = seq;  // the request: every input word above is written first
+    volatile uint64_t *word = reinterpret_cast<volatile uint64_t *>(c->hs_pin + host_word_off(n));
+    for (int launches = 0;;) {
+      if (!c->srv_running) {
+        // start a server, ordered after the work already on the caller's stream (e.g. a reset)
+        if (++launches > 2) return fail(HK_E_DEVICE, "hk_step_host: the step server exits without serving%s");
+        hk::StepIO s{};
+        s.actions = (const float *)c->hs_map;
+        s.opp_inc = (const double *)(c->hs_map + a_b);
+        uint8_t *o = c->hs_map + in_b;
+        s.obs = (float *)(o + kHostObs);
+        s.obs2 = (float *)(o + kHostObs2);
+        s.done = o + kHostDone;
+        s.record = (double *)(o + kHostRec);
+        hk::HostServer hs{};
+        hs.req = reinterpret_cast<const unsigned long long *>(c->hs_map + host_req_off(n));
+        hs.done = reinterpret_cast<unsigned long long *>(c->hs_map + host_word_off(n));
+        hs.args = reinterpret_cast<const int32_t *>(c->hs_map + host_args_off(n));
+        hs.idle_ticks = c->srv_idle_ticks;
+        hs.life_ticks = c->srv_life_ticks;
+        if ((e = hipEventRecord(c->srv_after, st)) != hipSuccess ||
+            (e = hipStreamWaitEvent(c->srv_stream, c->srv_after, 0)) != hipSuccess ||
+            (e = hk::launch_host_server(c->s, c->cfg, s, hs, c->srv_stream)) != hipSuccess)
+          return hipfail(e, "hk_step_host: server launch");
+        c->srv_running = true;
+        c->srv_start = std::chrono::steady_clock::now();
+      }
+      // Spin on the completion word; every 4096 polls ask the server's stream, so a server that faulted returns
+      // its error and one that exited on its own before serving this request is replaced.
+      uint32_t k = 1;
+      for (; *word != seq; ++k) {
+        if ((k & 4095u) == 0u) {
+          const hipError_t q = hipStreamQuery(c->srv_stream);
+          if (q == hipErrorNotReady) continue;
+          if (q != hipSuccess) {
+            c->srv_running = false;
+            return hipfail(q, "hk_step_host: step server");
+          }
+          if (*word == seq) break;
+          c->srv_running = false;  // exited (idle / life limit) without this request: start another
+          break;
+        }
+      }
+      if (*word == seq) break;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    c->srv_last = std::chrono::steady_clock::now();
+    std::memcpy(out, c->hs_pin + in_b, out_b);
+    return HK_OK;
+  }
   if (actions) std::memcpy(c->hs_pin, actions, a_b);
   if (opp_inc) std::memcpy(c->hs_pin + a_b, opp_inc, inc_b);
   uint8_t *dev = c->hs_staged ? c->hs_dev : c->hs_map;
@@ -284,6 +409,7 @@ int hk_get_state(void *ctx, float *state, int32_t *aux, void *stream) {
   if (!ctx) return fail(HK_E_INVALID, "hk_get_state: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_get_state");
   hipError_t e = hk::launch_get_state(c->s, c->cfg, state, aux, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_get_state");
 }
@@ -292,6 +418,7 @@ int hk_set_state(void *ctx, const uint8_t *mask, const float *state, const int32
   if (!ctx) return fail(HK_E_INVALID, "hk_set_state: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_set_state");
   hipError_t e = hk::launch_set_state(c->s, c->cfg, mask, state, aux, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_set_state");
 }
@@ -300,6 +427,7 @@ int hk_observe(void *ctx, float *obs, float *obs2, void *stream) {
   if (!ctx) return fail(HK_E_INVALID, "hk_observe: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_observe");
   hipError_t e = hk::launch_observe(c->s, c->cfg, obs, obs2, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_observe");
 }
@@ -308,6 +436,7 @@ int hk_info(void *ctx, double *info, double *info2, double *reward, double *rewa
   if (!ctx) return fail(HK_E_INVALID, "hk_info: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_info");
   hipError_t e = hk::launch_info(c->s, c->cfg, info, info2, reward, reward2, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_info");
 }
@@ -316,6 +445,7 @@ int hk_opponent_phase(void *ctx, double *phase_out, const double *phase_in, void
   if (!ctx) return fail(HK_E_INVALID, "hk_opponent_phase: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_opponent_phase");
   hipError_t e = hipSuccess;
   // device layout is [3][N] (player-major); the ABI layout is [N,2]
   if (phase_out)
@@ -337,6 +467,7 @@ int hk_opponent_phase3(void *ctx, double *phase_out, const double *phase_in, voi
   if (!ctx) return fail(HK_E_INVALID, "hk_opponent_phase3: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_opponent_phase3");
   hipError_t e = hipSuccess;
   // device layout is [3][N] (row-major by phase row); the ABI layout is [N,3]
   for (int r = 0; r < 3 && e == hipSuccess && phase_out; ++r)
@@ -352,6 +483,7 @@ int hk_counters(void *ctx, int64_t *out, void *stream) {
   if (!ctx || !out) return fail(HK_E_INVALID, "hk_counters: NULL argument%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_counters");
   hipError_t e = hipMemcpyAsync(out, c->s.counters, HK_NUM_COUNTERS * 8, hipMemcpyDeviceToHost, (hipStream_t)stream);
   if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_counters");
@@ -361,6 +493,7 @@ int hk_reset_counters(void *ctx, void *stream) {
   if (!ctx) return fail(HK_E_INVALID, "hk_reset_counters: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
+  HK_QUIESCE(c, "hk_reset_counters");
   hipError_t e = hipMemsetAsync(c->s.counters, 0, HK_NUM_COUNTERS * 8, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_reset_counters");
 }

@@ -53,7 +53,24 @@ struct StepIO {
   unsigned long long done_seq;
 };
 
+// hk_step_host's resident server (single-arena contexts): one wave stays on the GPU and serves step requests
+// posted in the context's mapped host buffer, so a step costs no launch.  Protocol (hk_capi.cpp hk_step_host):
+// the host writes the inputs and `args`, then the sequence number into `req` (release); the server sees
+// req != its last served number (acquire at system scope), runs the step with args' flags / input pointers,
+// writes the outputs and then the sequence number into `done` (release).  The server exits when `req` holds
+// kServerQuit, after idle_ticks of wall clock with no request, or after life_ticks in all -- every wave reaches
+// an exit, and the host relaunches a server on demand.
+constexpr unsigned long long kServerQuit = ~0ull;
+struct HostServer {
+  const unsigned long long *req;
+  unsigned long long *done;
+  const int32_t *args;  // [0] HK_STEP_* flags, [1] actions given, [2] phase increments given
+  unsigned long long idle_ticks, life_ticks;  // s_memrealtime (wall-clock counter) ticks
+};
+
 hipError_t launch_init(const DevState &s, const KCfg &cfg, hipStream_t st);
+hipError_t launch_host_server(const DevState &s, const KCfg &cfg, const StepIO &io, const HostServer &hs,
+                              hipStream_t st);
 hipError_t launch_reset(const DevState &s, const KCfg &cfg, const uint8_t *mask, const float *params,
                         const int32_t *max_t, const uint8_t *one, hipStream_t st);
 hipError_t launch_step(const DevState &s, const KCfg &cfg, const StepIO &io, int nsteps, hipStream_t st);

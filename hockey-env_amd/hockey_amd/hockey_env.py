@@ -15,6 +15,7 @@ before the call returns.  The fused
 reference's ``BasicOpponent`` (:785, :796), so seeded reference scripts reproduce.  ``render`` is out of scope.
 """
 import ctypes
+import struct
 import warnings
 
 import numpy as np
@@ -65,21 +66,23 @@ class _Snap:
         return self._aux
 
 
-def _clip4_into(dst, action):
-    """dst[0:4] = float32(np.clip(np.asarray(action, np.float64)[0:4], -1, 1)) (hockey_env.py:659, 875-886),
-    without numpy temporaries for the common inputs (a float ndarray or a list).  min(max(x, -1), 1) with x
-    first returns x for NaN and keeps -0.0, as np.clip does; the float32 store rounds like astype."""
+_PACK_ACT = struct.Struct("<8f").pack_into  # the 8 staged actions (float32, as astype rounds)
+_PACK_INC = struct.Struct("<d").pack_into
+
+
+def _stage_actions(buf, action):
+    """buf[0:8] (float32) = float32(np.clip(np.asarray(action, np.float64)[0:4], -1, 1)) followed by four zeros
+    (hockey_env.py:659, 875-886), packed in one call without numpy temporaries for the common inputs (a float
+    ndarray or a list of floats).  min(max(x, -1), 1) with x first returns x for NaN and keeps -0.0, as np.clip
+    does; the float32 pack rounds to nearest like astype."""
     if isinstance(action, np.ndarray) and action.dtype.kind == "f" and action.ndim == 1 and action.shape[0] >= 4:
         v = action[0:4].tolist()
     elif isinstance(action, (list, tuple)) and len(action) >= 4 and all(type(x) is float for x in action[0:4]):
-        v = action[0:4]
+        v = action
     else:
-        dst[0:4] = np.clip(np.asarray(action, np.float64)[0:4], -1, 1)
-        return
-    dst[0] = min(max(v[0], -1.0), 1.0)
-    dst[1] = min(max(v[1], -1.0), 1.0)
-    dst[2] = min(max(v[2], -1.0), 1.0)
-    dst[3] = min(max(v[3], -1.0), 1.0)
+        v = np.clip(np.asarray(action, np.float64)[0:4], -1, 1).tolist()
+    _PACK_ACT(buf, 0, min(max(v[0], -1.0), 1.0), min(max(v[1], -1.0), 1.0), min(max(v[2], -1.0), 1.0),
+              min(max(v[3], -1.0), 1.0), 0.0, 0.0, 0.0, 0.0)
 
 
 class HockeyEnv:
@@ -144,15 +147,9 @@ class HockeyEnv:
         return [seed]
 
     # --------------------------------------------------------------- device record
-    def _refresh(self, stepped):
-        """Decode the packed record.  After a step hk_step_host returned it in the host buffer; after a reset /
-        set_state the obs, info / rewards and aux of the current state are computed on the device and copied to
-        the host in one transfer."""
-        if stepped:
-            # obs2 / f stay views of the step's out buffer: the snapshot is replaced by the next step, which is the
-            # only writer of that buffer
-            self._snap = _Snap(self._out_obs.astype(np.float64), self._out_obs2, self._out_f)
-            return self._snap
+    def _refresh(self):
+        """The obs, info / rewards and aux of the current state after a reset / set_state: computed on the device
+        and copied to the host in one transfer (after a step, hk_step_host returned them; see _launch_step)."""
         L, ctx, st = self._vec.L, self._vec._ctx, self._vec._stream()
         p = self._ptr
         N.check(L.hk_observe(ctx, p["obs"], p["obs2"], st), "hk_observe")
@@ -185,7 +182,7 @@ class HockeyEnv:
         # max_t travels explicitly: the kernel's info / time limit follow the mode of THIS reset even after
         # the mode setter changed it (hockey_env.py:357-365)
         self._vec.reset_params(params[None, :], max_t=[max_t])
-        s = self._refresh(stepped=False)
+        s = self._refresh()
         return self._obs_out(s.obs), self._get_info()
 
     def _launch_step(self, a8, opp_inc=None):
@@ -201,12 +198,14 @@ class HockeyEnv:
         rc = self._step_fn(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._step_stream)
         if rc:
             N.check(rc, "hk_step_host")
-        s = self._refresh(stepped=True)
-        f = s.f
-        obs = s.obs if self.keep_mode else s.obs[:16].copy()  # a fresh float64 array either way
-        return obs, float(f[8]), bool(f[13]), False, {"winner": int(f[0]), "reward_closeness_to_puck": float(f[1]),
-                                                      "reward_touch_puck": float(f[2]),
-                                                      "reward_puck_direction": float(f[3])}
+        # the snapshot: obs2 / f stay views of the step's out buffer, which only
+        # the next step rewrites
+        o = self._out_obs.astype(np.float64)
+        self._snap = _Snap(o, self._out_obs2, self._out_f)
+        f = self._out_f.tolist()  # Python floats of the record (one conversion instead of one per field)
+        obs = o if self.keep_mode else o[:16].copy()  # a fresh float64 array either way
+        return obs, f[8], bool(f[13]), False, {"winner": int(f[0]), "reward_closeness_to_puck": f[1],
+                                               "reward_touch_puck": f[2], "reward_puck_direction": f[3]}
 
     def step(self, action):
         a = np.clip(np.asarray(action, np.float64), -1, +1).astype(np.float32)  # hockey_env.py:659
@@ -257,7 +256,7 @@ class HockeyEnv:
         if has is not None:
             aux[0], aux[1] = has
         self._vec.set_state(raw[None, :], aux[None, :])
-        self._refresh(stepped=False)
+        self._refresh()
 
     @property
     def time(self):
@@ -360,9 +359,8 @@ class HockeyEnv_BasicOpponent(HockeyEnv):
         # 0.0 + (0.2 - 0.0) * random_sample(), the same double as 0.2 * random() from the same global stream
         inc = 0.2 * np.random.random()
         self.opponent.phase += inc  # host mirror of the kernel's phase
-        _clip4_into(self._act_np, action)
-        self._act_np[4:8] = 0.0
-        self._inc_np[1] = inc
+        _stage_actions(self._act_np, action)
+        _PACK_INC(self._inc_np, 8, inc)
         return self._launch_step(None, opp_inc=True)
 
 

@@ -47,7 +47,7 @@ def test_facade_g2_step_laws_exact(golden):
             envs[(keep, mode)] = e
         env = envs[(keep, mode)]
         env._vec.set_state(g2["state"][i][None, :], g2["aux"][i][None, :])
-        env._refresh(stepped=False)
+        env._refresh()
         act = g2["action"][i]
         a = act if keep else np.concatenate([act[0:3], act[4:7]])
         obs, r, d, trunc, info = env.step(a)
@@ -111,7 +111,7 @@ def test_facade_set_state_g8(golden):
         keep = bool(g8["keep"][i])
         env = envs[int(keep)]
         env._vec.set_state(g8["raw_before"][i][None, :], np.zeros((1, 5), np.int32))
-        env._refresh(stepped=False)
+        env._refresh()
         env.set_state(g8["state"][i])
         st, _ = env._vec.get_state()
         assert np.array_equal(_np(st)[0], g8["raw_after"][i]), i
@@ -264,16 +264,17 @@ def test_hockey_one_seeded_run_vs_oracle(oracle):
     env.close()
 
 
-@pytest.mark.parametrize("staged", ["0", "1"])
-def test_step_host_on_fresh_contexts_equals_hk_step(monkeypatch, staged):
-    """hk_step_host (the facade's one-call step: mapped completion word, or HK_STEP_HOST_STAGED=1 copies) on
-    freshly created and destroyed single-arena contexts -- recycled pinned blocks included -- returns exactly what
-    hk_step returns on a twin context built the same way: obs, obs2, done and the float64 step record, from the
-    very first step on."""
+@pytest.mark.parametrize("staged,server", [("0", "1"), ("0", "0"), ("1", "0")])
+def test_step_host_on_fresh_contexts_equals_hk_step(monkeypatch, staged, server):
+    """hk_step_host (the facade's one-call step: the resident step server by default, one launch per step with a
+    mapped completion word under HK_STEP_HOST_SERVER=0, or HK_STEP_HOST_STAGED=1 copies) on freshly created and
+    destroyed single-arena contexts -- recycled pinned blocks included -- returns exactly what hk_step returns on a
+    twin context built the same way: obs, obs2, done and the float64 step record, from the very first step on."""
     from hockey_amd.hockey_env import HockeyEnv
 
     monkeypatch.setenv("HK_STEP_HOST_STAGED", staged)
-    rng = np.random.default_rng(int(staged))
+    monkeypatch.setenv("HK_STEP_HOST_SERVER", server)
+    rng = np.random.default_rng(int(staged) + 2 * int(server))
     for k in range(6):
         host, twin = HockeyEnv(), HockeyEnv()
         host.reset(seed=100 + k)
@@ -288,6 +289,51 @@ def test_step_host_on_fresh_contexts_equals_hk_step(monkeypatch, staged):
             assert np.array_equal(host._out_f, _np(res.record)[0]), (k, t)
         host.close()
         twin.close()
+
+
+def test_step_server_survives_idle_gaps_and_interleaved_calls(monkeypatch):
+    """The resident step server (hk_kernels.h HostServer) against the launch-per-step path on a twin facade: the
+    same actions through episodes with resets, set_state / get_state / observe calls between steps (each stops the
+    server first), pauses past the server's idle limit (it exits; the next step starts another) and a
+    kernel-counter read: every step's obs, obs2, record and the counters agree bit for bit."""
+    import time
+
+    from hockey_amd.hockey_env import HockeyEnv_BasicOpponent
+
+    envs = {}
+    for server in ("1", "0"):
+        monkeypatch.setenv("HK_STEP_HOST_SERVER", server)
+        np.random.seed(7)
+        envs[server] = HockeyEnv_BasicOpponent()
+    rng = np.random.default_rng(3)
+    np.random.seed(11)
+    st = np.random.get_state()
+    for ep in range(3):
+        for server, env in envs.items():
+            np.random.set_state(st)
+            env.reset(seed=40 + ep)
+        for t in range(60):
+            a = rng.uniform(-1, 1, 4)
+            res = {}
+            for server, env in envs.items():
+                np.random.set_state(st)
+                res[server] = env.step(a)
+            st = np.random.get_state()
+            o1, o0 = res["1"], res["0"]
+            assert np.array_equal(o1[0], o0[0]) and o1[1] == o0[1] and o1[2] == o0[2] and o1[4] == o0[4], (ep, t)
+            assert np.array_equal(envs["1"]._out_np, envs["0"]._out_np), (ep, t)
+            if t == 20:
+                time.sleep(0.05)  # past the server's 20 ms idle limit
+            if t == 30:
+                for env in envs.values():
+                    env._vec.get_state()  # a device call between steps
+                    env.set_state(o1[0])  # the state the last obs describes, on both twins
+            if o1[2]:
+                break
+    c = [env._vec.counters() for env in envs.values()]
+    assert np.array_equal(c[0], c[1]), c
+    for env in envs.values():
+        env.close()
 
 
 # ------------------------------------------------------------------------------------------------ behaviour

@@ -103,12 +103,12 @@ def test_source_hash_matches_makefile_recipe():
 
 
 def test_facade_action_staging_matches_numpy_clip():
-    """hockey_env._clip4_into (the facade's per-step action staging) stores exactly
+    """hockey_env._stage_actions (the facade's per-step action staging) stores exactly
     float32(np.clip(np.asarray(action, float64)[0:4], -1, 1)) (hockey_env.py:659, 875-886) for every input kind,
     including NaN, infinities, -0.0 and values that round across +-1 in float32."""
     import numpy as np
 
-    from hockey_amd.hockey_env import _clip4_into
+    from hockey_amd.hockey_env import _stage_actions
 
     rng = np.random.default_rng(0)
     cases = [rng.uniform(-3, 3, 4).astype(np.float32), rng.uniform(-3, 3, 8), rng.uniform(-1, 1, 6).astype(np.float16),
@@ -116,10 +116,11 @@ def test_facade_action_staging_matches_numpy_clip():
              (1.0000001, -1.0000001, 0.3, 0.2), [1, 2, 3, 4], np.array([1, 2, -3, 0], np.int64),
              np.array([[0.1, 0.2, 0.3, 0.4]]).reshape(4)]
     for c in cases:
-        got = np.zeros(8, np.float32)
-        _clip4_into(got, c)
+        got = np.full(8, 7.0, np.float32)
+        _stage_actions(got, c)
         want = np.clip(np.asarray(c, np.float64)[0:4], -1, 1).astype(np.float32)
         assert got[:4].view(np.uint32).tolist() == want.view(np.uint32).tolist(), (c, got, want)
+        assert got[4:].view(np.uint32).tolist() == [0, 0, 0, 0]
 
 
 def test_facade_phase_increment_is_the_reference_draw():
