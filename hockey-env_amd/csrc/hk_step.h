@@ -172,6 +172,39 @@ HK_DEV void store_arena(const Arena &w, const DevState &s, int64_t a) {
   I(s, I_ENABLED, a) = (int)w.enabled;
 }
 
+// store_arena after a step: the same words, but the fields that rarely change in play (sleep times, the puck's
+// pending force, awake bits, has_puck, done, winner, time limit, touching / enabled masks) are written only by
+// lanes whose value changed against the step's fetched words (fw, iw).  A wave whose 16 lanes of a 64-B segment
+// all keep their value issues no write for it, which takes those fields off the HBM write traffic.
+HK_DEV void store_arena_changed(const Arena &w, const DevState &s, int64_t a, const float *fw, const int32_t *iw) {
+  int awake = 0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int o = b * FB;
+    F(s, o + FB_PX, a) = w.d.px[b];
+    F(s, o + FB_PY, a) = w.d.py[b];
+    F(s, o + FB_CX, a) = w.d.cx[b];
+    F(s, o + FB_CY, a) = w.d.cy[b];
+    F(s, o + FB_A, a) = w.d.a[b];
+    F(s, o + FB_VX, a) = w.d.vx[b];
+    F(s, o + FB_VY, a) = w.d.vy[b];
+    F(s, o + FB_W, a) = w.d.w[b];
+    if (__float_as_uint(w.d.sleep[b]) != __float_as_uint(fw[o + FB_SLEEP])) F(s, o + FB_SLEEP, a) = w.d.sleep[b];
+    awake |= (w.d.awake[b] & 1) << b;
+  }
+  if (__float_as_uint(w.d.fx[B_PK]) != __float_as_uint(fw[F_PFX])) F(s, F_PFX, a) = w.d.fx[B_PK];
+  if (__float_as_uint(w.d.fy[B_PK]) != __float_as_uint(fw[F_PFY])) F(s, F_PFY, a) = w.d.fy[B_PK];
+  if (awake != iw[I_AWAKE]) I(s, I_AWAKE, a) = awake;
+  if (w.has1 != iw[I_HAS1]) I(s, I_HAS1, a) = w.has1;
+  if (w.has2 != iw[I_HAS2]) I(s, I_HAS2, a) = w.has2;
+  I(s, I_TIME, a) = w.time;
+  if (w.done != iw[I_DONE]) I(s, I_DONE, a) = w.done;
+  if (w.winner != iw[I_WINNER]) I(s, I_WINNER, a) = w.winner;
+  if (w.max_t != iw[I_MAXT]) I(s, I_MAXT, a) = w.max_t;
+  if ((int)w.touch != iw[I_TOUCH]) I(s, I_TOUCH, a) = (int)w.touch;
+  if ((int)w.enabled != iw[I_ENABLED]) I(s, I_ENABLED, a) = (int)w.enabled;
+}
+
 // HockeyEnv.reset body re-creation (hockey_env.py:345-418) from placement params.
 // player*_has_puck is NOT cleared (the reference's reset never assigns it).
 HK_DEV void reset_arena(Arena &w, const float *p6, int max_t) {
@@ -416,7 +449,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     observe_two(w, o);
     for (int k = 0; k < 18; ++k) io.obs2[a * 18 + k] = o[k];
   }
-  store_arena(w, s, a);
+  store_arena_changed(w, s, a, m.f, m.i);
   I(s, I_STEP, a) = (int)(stepc + 1);
   HK_TIC(T, 12);  // diagnostics: outputs and state store
   out.done_edge = done_edge;

@@ -141,11 +141,18 @@ int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t 
 int hk_step(void *ctx, const hk_step_io *io, void *stream);
 
 /* HockeyEnv.step of a SINGLE-arena context with host buffers: the reference's deployment shape (one env, numpy
- * in and out, hockey_env.py:658-695) in one call -- the action (and BasicOpponent phase increments) are staged
- * through pinned memory, the step kernel runs on `stream`, and the packed result returns to `out` before the
- * call returns (the host waits on a completion word the kernel stores after its last output, not on the stream).  actions: host [1,8] f32 (NULL if no player is external); opp_inc: host
- * [1,2] f64 or NULL; flags: HK_STEP_* (as hk_step_io.flags); out: host buffer of HK_HOST_RECORD_BYTES = obs f32[18] @0, obs2 f32[18] @72, done u8 @144,
- * hk_step_io.record f64[16] @152.  HK_E_INVALID for a context with more than one arena. */
+ * in and out, hockey_env.py:658-695) in one call.  The action (and BasicOpponent phase increments) go through
+ * the context's pinned, device-mapped buffer and the packed result returns to `out` before the call returns.
+ * By default a resident step server does the step: a one-wave kernel that stays on the GPU on a private stream
+ * (started on the first call, ordered after the work already on `stream`) and serves each call's request from
+ * the mapped buffer, so a step costs no kernel launch.  It exits after 20 ms without a request or 2 s in all and
+ * is restarted on demand; every other entry point of the context stops it first, so context calls stay ordered
+ * as on one stream.  HK_STEP_HOST_SERVER=0 launches one step kernel per call on `stream` instead (the host waits
+ * on a completion word the kernel stores after its last output); HK_STEP_HOST_STAGED=1 stages through device
+ * copies (A/B timing).  actions: host [1,8] f32 (NULL if no player is external); opp_inc: host [1,2] f64 or
+ * NULL; flags: HK_STEP_* (as hk_step_io.flags); out: host buffer of HK_HOST_RECORD_BYTES = obs f32[18] @0,
+ * obs2 f32[18] @72, done u8 @144, hk_step_io.record f64[16] @152.  HK_E_INVALID for a context with more than
+ * one arena. */
 #define HK_HOST_RECORD_BYTES 280
 int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t flags, void *out, void *stream);
 
