@@ -287,7 +287,41 @@ HK_DEV void device_placement(uint64_t seed, int64_t a, uint32_t episode, int mod
 }
 
 HK_DEV void write_info(float *dst, int64_t a, const double *info) {
-  for (int k = 0; k < 4; ++k) dst[a * 4 + k] = (float)info[k];
+  float *p = dst + a * 4;
+  if (((uintptr_t)p & 15) == 0) {  // one 16-B store: the lane's row is written whole, no partial-line write
+    *reinterpret_cast<float4 *>(p) = float4{(float)info[0], (float)info[1], (float)info[2], (float)info[3]};
+  } else {
+    for (int k = 0; k < 4; ++k) p[k] = (float)info[k];
+  }
+}
+
+// This lane's K-float output row (arena a, row-major [N][K]).  Device build, full wave with a 16-B-aligned wave
+// block: the 64 rows are staged in the wave's free LDS work-list area and written as 16-B stores of consecutive
+// memory, so each store instruction writes whole 64-B segments (a per-lane dword store covers every row of the
+// wave at one word, and the L2 then writes each line piecewise).  Otherwise per-lane stores.
+template <int K>
+HK_DEV void store_row(float *dst, int64_t a, const float *v, float *stage, int lane) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(64 * K <= kToiQ * kToiItemWords, "the staged rows fit the TOI work-list area");
+  float *base = dst + (a - lane) * K;
+  if (__ballot(1) == ~0ull && ((uintptr_t)base & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) stage[lane * K + j] = v[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float4 *src = reinterpret_cast<const float4 *>(stage);
+    float4 *d4 = reinterpret_cast<float4 *>(base);
+#pragma unroll
+    for (int q = 0; q < (16 * K + 63) / 64; ++q)
+      if (q * 64 + lane < 16 * K) d4[q * 64 + lane] = src[q * 64 + lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the stage is free again for the next row
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return;
+  }
+#endif
+  for (int j = 0; j < K; ++j) dst[a * K + j] = v[j];
 }
 
 // HockeyEnv.reset of arena a: explicit placement params or device placement (Philox), one_starting toggle.
@@ -443,11 +477,11 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     I(s, I_EPISODE, a) = (int)(ep + 1);
     observe(w, o);
   }
-  if (io.obs)
-    for (int k = 0; k < 18; ++k) io.obs[a * 18 + k] = o[k];
+  float *stage = lds + kLdsPerLane * 64;  // the TOI / narrow-phase work-list area, free after world_step
+  if (io.obs) store_row<18>(io.obs, a, o, stage, lane);
   if (io.obs2) {
     observe_two(w, o);
-    for (int k = 0; k < 18; ++k) io.obs2[a * 18 + k] = o[k];
+    store_row<18>(io.obs2, a, o, stage, lane);
   }
   store_arena_changed(w, s, a, m.f, m.i);
   I(s, I_STEP, a) = (int)(stepc + 1);

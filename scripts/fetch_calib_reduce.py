@@ -35,11 +35,13 @@ def main():
     for k, (r, w) in known.items():
         f, wr = fetch.get(k), write.get(k)
         out["kernels"][k] = {"known_read": r, "known_write": w, "fetch_size_bytes": f, "write_size_bytes": wr,
+                             "fetch_per_written_byte": f / w if f is not None and w else None,
                              "fetch_over_known": f / r if f is not None and r else None,
                              "write_over_known": wr / w if wr is not None and w else None}
         print(f"{k:12s} read {r:10d} FETCH {f if f is None else round(f):>10}  ratio "
               f"{out['kernels'][k]['fetch_over_known']}  | write {w:10d} WRITE {wr if wr is None else round(wr):>10}  "
-              f"ratio {out['kernels'][k]['write_over_known']}")
+              f"ratio {out['kernels'][k]['write_over_known']}  | FETCH per byte written "
+              f"{out['kernels'][k]['fetch_per_written_byte']}")
     os.makedirs(os.path.join(ROOT, "profiles", "r04"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "r04", "fetch_calib.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -8,6 +8,10 @@
 //   soa_quad    4 x 16-B quads per lane read and written (the guide's calibrated case: 16 B per lane)
 //   byte_store  1 byte per lane written (done), 1 float per lane written (reward), nothing read
 //   rec_sparse  64-B records [N][16] read (3 quads) and written (4 quads) by 40 % of lanes (the manifold records)
+//   obs_dword   [N][18] floats written as 18 dword stores per lane (the step kernel's obs rows: a store
+//               instruction covers every 72-B row of the wave at one word, so each 128-B line is written piecewise)
+//   obs_lds     the same rows staged through LDS and written as 16-B stores of consecutive wave memory
+//   info_dword  [N][4] floats as 4 dword stores per lane;  info_quad  the same as one 16-B store per lane
 // Build: hipcc --offload-arch=gfx950 -O3 -o fetch_calib fetch_calib.hip.  Run each counter in its own pass:
 //   rocprofv3 --pmc FETCH_SIZE -d DIR -o run --output-format csv -- ./fetch_calib
 // scripts/fetch_calib_reduce.py divides each kernel's counter by its known bytes.
@@ -65,6 +69,31 @@ __global__ void rec_sparse(float4 *__restrict__ rec) {
   r[3] = q0;
 }
 
+__global__ void obs_dword(float *__restrict__ obs) {
+  const int a = blockIdx.x * 64 + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 18; ++k) obs[(size_t)a * 18 + k] = (float)(a + k);
+}
+__global__ void obs_lds(float *__restrict__ obs) {
+  __shared__ float st[64 * 18];
+  const int t = threadIdx.x, a0 = blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 18; ++k) st[t * 18 + k] = (float)(a0 + t + k);
+  __syncthreads();
+  const float4 *src = reinterpret_cast<const float4 *>(st);
+  float4 *dst = reinterpret_cast<float4 *>(obs + (size_t)a0 * 18);
+  for (int j = t; j < 64 * 18 / 4; j += 64) dst[j] = src[j];
+}
+__global__ void info_dword(float *__restrict__ info) {
+  const int a = blockIdx.x * 64 + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) info[(size_t)a * 4 + k] = (float)(a + k);
+}
+__global__ void info_quad(float4 *__restrict__ info) {
+  const int a = blockIdx.x * 64 + threadIdx.x;
+  info[a] = float4{(float)a, (float)(a + 1), (float)(a + 2), (float)(a + 3)};
+}
+
 #define CK(x)                                                                   \
   do {                                                                          \
     hipError_t e_ = (x);                                                        \
@@ -79,7 +108,7 @@ int main() {
   double *din, *dout;
   float4 *qin, *qout, *rec;
   unsigned char *done;
-  float *rew;
+  float *rew, *obs, *info;
   CK(hipMalloc(&fin, sizeof(float) * NF * N));
   CK(hipMalloc(&fout, sizeof(float) * NF * N));
   CK(hipMalloc(&din, sizeof(double) * 3 * N));
@@ -89,6 +118,8 @@ int main() {
   CK(hipMalloc(&rec, sizeof(float4) * 4 * N));
   CK(hipMalloc(&done, N));
   CK(hipMalloc(&rew, sizeof(float) * N));
+  CK(hipMalloc(&obs, sizeof(float) * 18 * N));
+  CK(hipMalloc(&info, sizeof(float) * 4 * N));
   CK(hipMemset(fin, 0, sizeof(float) * NF * N));
   CK(hipMemset(din, 0, sizeof(double) * 3 * N));
   CK(hipMemset(qin, 0, sizeof(float4) * 4 * N));
@@ -101,6 +132,10 @@ int main() {
   for (int r = 0; r < REPS; ++r) soa_quad<<<g, b>>>(qin, qout);
   for (int r = 0; r < REPS; ++r) byte_store<<<g, b>>>(done, rew);
   for (int r = 0; r < REPS; ++r) rec_sparse<<<g, b>>>(rec);
+  for (int r = 0; r < REPS; ++r) obs_dword<<<g, b>>>(obs);
+  for (int r = 0; r < REPS; ++r) obs_lds<<<g, b>>>(obs);
+  for (int r = 0; r < REPS; ++r) info_dword<<<g, b>>>(info);
+  for (int r = 0; r < REPS; ++r) info_quad<<<g, b>>>(reinterpret_cast<float4 *>(info));
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
   int touched = 0;
@@ -112,7 +147,11 @@ int main() {
   printf("soa_quad %d %d\n", 4 * N * 16, 4 * N * 16);
   printf("byte_store %d %d\n", 0, N * 5);
   printf("rec_sparse %d %d\n", touched * 48, touched * 64);
+  printf("obs_dword %d %d\n", 0, N * 72);
+  printf("obs_lds %d %d\n", 0, N * 72);
+  printf("info_dword %d %d\n", 0, N * 16);
+  printf("info_quad %d %d\n", 0, N * 16);
   hipFree(fin); hipFree(fout); hipFree(din); hipFree(dout); hipFree(qin); hipFree(qout); hipFree(rec);
-  hipFree(done); hipFree(rew);
+  hipFree(done); hipFree(rew); hipFree(obs); hipFree(info);
   return 0;
 }
