@@ -579,14 +579,25 @@ __global__ void __launch_bounds__(256) adam_kernel(hkl_adam_io io) {
     const int64_t k = e - base;
     const int64_t rr = k / S.cols, cc = k % S.cols;
     const float *src = S.src + rr * S.ld + cc;
-    float p8[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    int c = 0;
-    for (; c + 8 <= S.chunks; c += 8) {
+    // 16 partial sums: 16 slab loads in flight per thread (the reduction is bound by memory-level parallelism:
+    // ~2 workgroups per CU at the C5 parameter counts), summed in a fixed tree
+    float p16[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) p8[u] += src[(int64_t)(c + u) * S.stride];
+    for (int u = 0; u < 16; ++u) p16[u] = 0.0f;
+    int c = 0;
+    for (; c + 16 <= S.chunks; c += 16) {
+      float q[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) q[u] = src[(int64_t)(c + u) * S.stride];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p16[u] += q[u];
     }
-    for (; c < S.chunks; ++c) p8[0] += src[(int64_t)c * S.stride];
-    float g = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
+    for (; c < S.chunks; ++c) p16[c & 15] += src[(int64_t)c * S.stride];
+#pragma unroll
+    for (int h = 8; h >= 1; h >>= 1)
+#pragma unroll
+      for (int u = 0; u < h; ++u) p16[u] = p16[u] + p16[u + h];
+    float g = p16[0];
     float p = S.param[k];
     if (io.wd != 0.0f) g += io.wd * p;
     const float t = (float)(*io.step + 1);
@@ -600,11 +611,23 @@ __global__ void __launch_bounds__(256) adam_kernel(hkl_adam_io io) {
     S.v[k] = v;
     S.param[k] = p;
   }
-  if (e == 0 && io.loss_src) {  // the step's loss: sum of the workgroup partials / batch, into the learner's accumulator
+  if (blockIdx.x == 0 && io.loss_src) {
+    // the step's loss: the sum of the workgroup partials (scaled), into the learner's accumulator -- a fixed-order
+    // tree over workgroup 0's 256 threads (one thread summing 256 dependent loads was this kernel's tail)
+    __shared__ float lred[256];
     float s = 0.0f;
-    for (int c = 0; c < io.loss_chunks; ++c) s += io.loss_src[c];
-    *io.loss_sum += (double)(s * io.loss_scale);
-    *io.loss_count += 1.0;
+    for (int c = threadIdx.x; c < io.loss_chunks; c += 256) s += io.loss_src[c];
+    lred[threadIdx.x] = s;
+    __syncthreads();
+#pragma unroll
+    for (int h = 128; h >= 1; h >>= 1) {
+      if ((int)threadIdx.x < h) lred[threadIdx.x] = lred[threadIdx.x] + lred[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      *io.loss_sum += (double)(lred[0] * io.loss_scale);
+      *io.loss_count += 1.0;
+    }
   }
 }
 

@@ -241,12 +241,14 @@ def test_facades_drop_in(golden):
 
 
 @pytest.mark.gpu
-def test_rollout_equals_repeated_steps():
+@pytest.mark.parametrize("n", [512, 37])
+def test_rollout_equals_repeated_steps(n):
     """hk_rollout(K) == K hk_step calls, bit for bit: per-step outputs, final state and counters
-    (fused opponents + auto-reset, and external actions)."""
+    (fused opponents + auto-reset, and external actions).  512 arenas write their observation rows as staged
+    16-B stores of whole waves; 37 (one partial wave) takes the per-lane stores."""
     import torch
 
-    n, k = 512, 37
+    k = 37
     for pol in (("strong", "weak"), ("external", "strong")):
         a = _vec(n, policies=pol, auto_reset=True, seed=11)
         b = _vec(n, policies=pol, auto_reset=True, seed=11)
