@@ -44,6 +44,9 @@ def main():
                          "500-step loop (hockey_amd.td3.train docstring)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "r03", "stage1_pin.json"))
     ap.add_argument("--checkpoint", default=None, help="save the final agent (reference td3_*.pt layout) here")
+    ap.add_argument("--learner", choices=["auto", "fused", "eager"], default="auto",
+                    help="hockey_amd.td3.train's learner: the fused MFMA kernels (auto: on the GPU from batch 256) "
+                         "or the eager PyTorch update (r03's runs)")
     args = ap.parse_args()
     cfg = TD3Config.from_json(os.path.join(ROOT, "tests", "golden", "stage1_config.json"))
     n = args.arenas
@@ -51,7 +54,7 @@ def main():
     dev = "cuda:0"
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     out = {"config": vars(cfg), "arenas": n, "rounds": rounds, "episodes": rounds * n, "seed": args.seed,
-           "episode_end": args.episode_end,
+           "episode_end": args.episode_end, "learner": args.learner,
            "updates_per_round": updates_for(cfg, n, cfg.max_steps), "eval_episodes": args.eval_episodes,
            "reference_wr_weak": REF_WR_WEAK, "evals": []}
     t_start = time.time()
@@ -89,8 +92,9 @@ def main():
         print(json.dumps(rec), flush=True)
         return rec
 
+    fused = {"auto": "auto", "fused": True, "eager": False}[args.learner]
     agent, st = train(n_arenas=n, rounds=rounds, cfg=cfg, device=dev, seed=args.seed, eval_fn=eval_fn,
-                      graphs=not args.no_graphs, episode_end=args.episode_end, log=log)
+                      graphs=not args.no_graphs, episode_end=args.episode_end, log=log, fused=fused)
     torch.cuda.synchronize()
     wr = [e["wr_weak"] for e in out["evals"]]
     first = next((e for e in out["evals"] if e["wr_weak"] >= 0.9), None)
