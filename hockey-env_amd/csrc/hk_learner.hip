@@ -471,14 +471,16 @@ struct WgJobs {
   WgJob job[4];
   int chunks, chunk_size;
 };
+constexpr int kWgSub = 32, kWgOt = 128, kWgPad = 4;
+// One split-K tile of dW = DZ^T X: output rows [o0, o0 + 128) x k columns [k0, k0 + KT) of job jb, summed over one
+// chunk of samples (sa / sb: this block's double-buffered LDS staging, [2][32][128 + 4] and [2][32][KT + 4]).
 template <int KT>
-__global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
-  constexpr int SUB = 32, OT = 128, PAD = 4;
+__device__ __forceinline__ void wgrad_tile(const WgJobs &jobs, int bx, int by, int bz, float (*sa)[kWgSub][kWgOt + kWgPad],
+                                           float (*sb)[kWgSub][KT + kWgPad]) {
+  constexpr int SUB = kWgSub, OT = kWgOt;
   constexpr int NB = KT == 128 ? 4 : 1;  // 16-column blocks per wave
   constexpr int LA = SUB * OT / 4 / WG, LB = (SUB * KT / 4 + WG - 1) / WG;  // f4 loads per thread per sub-chunk
-  __shared__ float sa[2][SUB][OT + PAD];
-  __shared__ float sb[2][SUB][KT + PAD];
-  const int jb = blockIdx.z / jobs.chunks, chunk = blockIdx.z % jobs.chunks;
+  const int jb = bz / jobs.chunks, chunk = bz % jobs.chunks;
   const float *__restrict__ dz = jobs.job[jb].dz;
   const float *__restrict__ xs = jobs.job[jb].x;
   float *__restrict__ slab = jobs.job[jb].slab;
@@ -486,10 +488,10 @@ __global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
   const int ldx = jobs.job[jb].ldx;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, kk = lane >> 4, i = lane & 15;
   const int wo = wave >> 1, wk = wave & 1;
-  const int o0 = blockIdx.x * OT, k0 = blockIdx.y * KT;
+  const int o0 = bx * OT, k0 = by * KT;
   const int csize = jobs.chunk_size;
   const int64_t j0 = (int64_t)chunk * csize;
-  const bool bias = bslab != nullptr && blockIdx.y == 0;
+  const bool bias = bslab != nullptr && by == 0;
   f4 acc[4][NB];
 #pragma unroll
   for (int bo = 0; bo < 4; ++bo)
@@ -557,6 +559,30 @@ __global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
         dst[(int64_t)o * ldx + k0 + 16 * wk + i] = acc[bo][0][r];
       }
     }
+}
+
+template <int KT>
+__global__ void __launch_bounds__(WG, 1) wgrad_kernel(WgJobs jobs) {
+  __shared__ float sa[2][kWgSub][kWgOt + kWgPad];
+  __shared__ float sb[2][kWgSub][KT + kWgPad];
+  wgrad_tile<KT>(jobs, blockIdx.x, blockIdx.y, blockIdx.z, sa, sb);
+}
+
+// hkl_wgrad_pair: a network's dW2 tiles (k width 256) and dW1 tiles (k width 32) in one launch -- blocks
+// [0, n_wide) take the wide jobs (grid 2 x 2 x chunks per job), the rest the narrow ones (2 x 1 x chunks), so the
+// short dW1 tiles fill the SIMDs the dW2 tiles leave and one launch gap is saved.  The narrow tile's staging
+// lives inside the wide one's (same LDS as a wide-only block).
+__global__ void __launch_bounds__(WG, 1) wgrad_pair_kernel(WgJobs wide, WgJobs narrow, int n_wide) {
+  __shared__ float sa[2][kWgSub][kWgOt + kWgPad];
+  __shared__ float sb[2][kWgSub][128 + kWgPad];
+  static_assert(sizeof(float[2][kWgSub][XP + kWgPad]) <= sizeof(sb), "the narrow staging fits the wide one");
+  const int id = blockIdx.x;
+  if (id < n_wide) {
+    wgrad_tile<128>(wide, id & 1, (id >> 1) & 1, id >> 2, sa, sb);
+  } else {
+    const int j = id - n_wide;
+    wgrad_tile<XP>(narrow, j & 1, 0, j >> 1, sa, reinterpret_cast<float(*)[kWgSub][XP + kWgPad]>(&sb[0][0][0]));
+  }
 }
 
 // ------------------------------------------------------------------------------------------------ Adam
@@ -778,6 +804,25 @@ int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch,
   else hipLaunchKernelGGL(wgrad_kernel<32>, dim3(2, 1, z), dim3(WG), 0, (hipStream_t)stream, J);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? HKL_OK : fail(e, "hkl_wgrad");
+}
+
+static WgJobs wg_jobs(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch) {
+  WgJobs J{};
+  for (int k = 0; k < n_jobs; ++k) J.job[k] = WgJob{jobs[k].dz, jobs[k].x, jobs[k].slab, jobs[k].bias_slab, k_width};
+  J.chunk_size = (k_width == 256 && batch % 512 == 0) ? 512 : 256;
+  J.chunks = (int)(batch / J.chunk_size);
+  return J;
+}
+
+int hkl_wgrad_pair(const hkl_wgrad_job *wide, int n_wide, const hkl_wgrad_job *narrow, int n_narrow, int64_t batch,
+                   void *stream) {
+  if (!wide || !narrow || n_wide < 1 || n_wide > 4 || n_narrow < 1 || n_narrow > 4 || batch <= 0 || batch % CHUNK)
+    return HKL_E_INVALID;
+  const WgJobs W = wg_jobs(wide, n_wide, 256, batch), N = wg_jobs(narrow, n_narrow, XP, batch);
+  const int nw = 4 * W.chunks * n_wide, nn = 2 * N.chunks * n_narrow;
+  hipLaunchKernelGGL(wgrad_pair_kernel, dim3((unsigned)(nw + nn)), dim3(WG), 0, (hipStream_t)stream, W, N, nw);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? HKL_OK : fail(e, "hkl_wgrad_pair");
 }
 
 int hkl_adam(const hkl_adam_io *io, void *stream) {

@@ -74,6 +74,7 @@ class AdamIO(ctypes.Structure):
 
 
 EXPORTS = ["hkl_last_error", "hkl_pack_floats", "hkl_pack", "hkl_critic_step", "hkl_actor_step", "hkl_wgrad",
+           "hkl_wgrad_pair",
            "hkl_adam", "hkl_polyak", "hkl_tanh_probe", "hkl_sample"]
 
 
@@ -100,6 +101,8 @@ def lib():
         L.hkl_critic_step.argtypes = [ctypes.POINTER(CriticIO), vp]
         L.hkl_actor_step.argtypes = [ctypes.POINTER(ActorIO), vp]
         L.hkl_wgrad.argtypes = [ctypes.POINTER(WgJob), ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp]
+        L.hkl_wgrad_pair.argtypes = [ctypes.POINTER(WgJob), ctypes.c_int, ctypes.POINTER(WgJob), ctypes.c_int,
+                                     ctypes.c_int64, vp]
         L.hkl_adam.argtypes = [ctypes.POINTER(AdamIO), vp]
         L.hkl_polyak.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_float, ctypes.c_float, vp]
         L.hkl_tanh_probe.argtypes = [vp, vp, ctypes.c_int64, vp]
@@ -322,8 +325,7 @@ class FusedLearner:
             iw = (1.0 / (p * self.ring.size_t)) ** self.ring.beta
             self.iw.copy_(iw / iw.max())
         _check(L.hkl_critic_step(ctypes.byref(self.cio), st), "hkl_critic_step")
-        _check(L.hkl_wgrad(self.wg["c256"], 2, 256, self.B, st), "hkl_wgrad")
-        _check(L.hkl_wgrad(self.wg["c32"], 2, XP, self.B, st), "hkl_wgrad")
+        _check(L.hkl_wgrad_pair(self.wg["c256"], 2, self.wg["c32"], 2, self.B, st), "hkl_wgrad_pair")
         _check(L.hkl_adam(ctypes.byref(self.adam["critic"]), st), "hkl_adam")
         self._pack([self.nets["q1"], self.nets["q2"]], self.step["critic"], st)
         if self.ring.prioritized:
@@ -332,8 +334,7 @@ class FusedLearner:
         if not train_actor:
             return
         _check(L.hkl_actor_step(ctypes.byref(self.aio), st), "hkl_actor_step")
-        _check(L.hkl_wgrad(self.wg["a256"], 1, 256, self.B, st), "hkl_wgrad")
-        _check(L.hkl_wgrad(self.wg["a32"], 1, XP, self.B, st), "hkl_wgrad")
+        _check(L.hkl_wgrad_pair(self.wg["a256"], 1, self.wg["a32"], 1, self.B, st), "hkl_wgrad_pair")
         _check(L.hkl_adam(ctypes.byref(self.adam["actor"]), st), "hkl_adam")
         self._pack([self.nets["actor"]], self.step["actor"], st)
         ta, tc = c.tau_actor, c.tau_critic

@@ -104,6 +104,10 @@ typedef struct {
 } hkl_wgrad_job;
 /* 1..4 jobs of one k_width (256 or 32) in one launch */
 int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch, void *stream);
+/* hkl_wgrad for n_wide k-width-256 jobs (dW2) and n_narrow k-width-32 jobs (dW1) in one launch (the same slabs as
+ * the two hkl_wgrad calls, bit for bit). */
+int hkl_wgrad_pair(const hkl_wgrad_job *wide, int n_wide, const hkl_wgrad_job *narrow, int n_narrow, int64_t batch,
+                   void *stream);
 int hkl_adam(const hkl_adam_io *io, void *stream);
 /* target = target * rho + tau * param over n floats (soft_update; tau = 1 - rho) */
 int hkl_polyak(float *target, const float *param, int64_t n, float rho, float tau, void *stream);

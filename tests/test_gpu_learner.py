@@ -199,3 +199,41 @@ def test_device_sampling_distribution():
     assert abs(float(inner.mean())) < 0.003
     clip_share = float((z.abs() >= 0.3 - 1e-7).double().mean())
     assert abs(clip_share - 0.1336) < 0.01, clip_share  # P(|N(0, 0.2)| > 0.3) = 2 (1 - Phi(1.5))
+
+
+def test_wgrad_pair_equals_two_wgrad_launches():
+    """hkl_wgrad_pair (dW2 and dW1 tiles of the critics in one launch) writes exactly the slabs -- weight and bias
+    column sums -- that one hkl_wgrad call per k width writes."""
+    import ctypes
+
+    from hockey_amd.learner_hip import XP, WgJob, _p, lib
+
+    L = lib()
+    B, H = 1024, 256
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dz2 = [torch.randn(B, H, device=DEV, generator=g) for _ in range(2)]
+    h1 = [torch.randn(B, H, device=DEV, generator=g) for _ in range(2)]
+    dz1 = [torch.randn(B, H, device=DEV, generator=g) for _ in range(2)]
+    x0 = torch.randn(B, XP, device=DEV, generator=g)
+    C, C1 = B // 512, B // 256
+    outs = []
+    for pair in (False, True):
+        s2 = [torch.full((C, H, H), 7.0, device=DEV) for _ in range(2)]
+        b2 = [torch.full((C, H), 7.0, device=DEV) for _ in range(2)]
+        s1 = [torch.full((C1, H, XP), 7.0, device=DEV) for _ in range(2)]
+        b1 = [torch.full((C1, H), 7.0, device=DEV) for _ in range(2)]
+        wide = (WgJob * 2)(*[WgJob(_p(dz2[k]), _p(h1[k]), _p(s2[k]), _p(b2[k])) for k in range(2)])
+        narrow = (WgJob * 2)(*[WgJob(_p(dz1[k]), _p(x0), _p(s1[k]), _p(b1[k])) for k in range(2)])
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        if pair:
+            assert L.hkl_wgrad_pair(wide, 2, narrow, 2, B, st) == 0
+        else:
+            assert L.hkl_wgrad(wide, 2, 256, B, st) == 0
+            assert L.hkl_wgrad(narrow, 2, XP, B, st) == 0
+        torch.cuda.synchronize()
+        outs.append(s2 + b2 + s1 + b1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # and they are the weight gradients: chunk sums of DZ^T X
+    ref = dz2[0].double().T @ h1[0].double()
+    assert torch.allclose(outs[1][0].double().sum(0), ref, rtol=1e-4, atol=1e-3)
