@@ -281,8 +281,14 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
       int khz = 0;
       if ((e = hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking)) != hipSuccess ||
           (e = hipEventCreateWithFlags(&c->srv_after, hipEventDisableTiming)) != hipSuccess ||
-          (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device)) != hipSuccess)
-        return hipfail(e, "hk_step_host: server stream");
+          (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device)) != hipSuccess || khz <= 0) {
+        // no server for this context: its steps take the launch-per-step path (still the GPU kernel)
+        if (c->srv_stream) (void)hipStreamDestroy(c->srv_stream);
+        if (c->srv_after) (void)hipEventDestroy(c->srv_after);
+        c->srv_stream = nullptr;
+        c->srv_after = nullptr;
+        c->srv_on = 0;
+      }
       c->srv_idle_ticks = (unsigned long long)khz * kSrvIdleMs;
       c->srv_life_ticks = (unsigned long long)khz * kSrvLifeMs;
     }
