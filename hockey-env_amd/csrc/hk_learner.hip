@@ -9,8 +9,9 @@
 //                 action and through the actor (update_actor, :138-175) -- one launch;
 //   wgrad         the weight gradients dW = dZ^T X (the reduction over the batch) as split-K MFMA tiles;
 //   adam          per-parameter reduction of the gradient slabs in a fixed order + torch.optim.Adam's update
-//                 (lr, betas (0.9, 0.999), eps, L2 weight decay; rl/td3/agent.py:174-182);
-//   polyak        soft_update (:196-218), then pack re-lays the changed weights out for the MFMA operands.
+//                 (lr, betas (0.9, 0.999), eps, L2 weight decay; rl/td3/agent.py:174-182), on actor updates with
+//                 soft_update (:196-218) folded in;
+//   pack          re-lays the changed weights out for the MFMA operands (polyak: soft_update as its own launch).
 //
 // Every product is v_mfma_f32_16x16x4_f32: exact f32 fma chains (no reduced-precision path on gfx950), so the
 // arithmetic is the reference's fp32 up to summation order.  Layout of a wave's activations ("Tile"): lane l holds
@@ -636,6 +637,8 @@ __global__ void __launch_bounds__(256) adam_kernel(hkl_adam_io io) {
     S.m[k] = m;
     S.v[k] = v;
     S.param[k] = p;
+    if (io.polyak && S.target)  // soft_update with the new parameter: target.mul_(rho).add_(tau * param)
+      S.target[k] = __fadd_rn(__fmul_rn(S.target[k], io.polyak_rho), __fmul_rn(io.polyak_tau, p));
   }
   if (blockIdx.x == 0 && io.loss_src) {
     // the step's loss: the sum of the workgroup partials (scaled), into the learner's accumulator -- a fixed-order
@@ -767,7 +770,7 @@ extern "C" {
 const char *hkl_last_error(void) { return g_err; }
 
 int hkl_pack(const hkl_net *nets, int n_nets, int64_t *step, void *stream) {
-  if (n_nets < 1 || n_nets > 3) return HKL_E_INVALID;
+  if (n_nets < 1 || n_nets > 4) return HKL_E_INVALID;
   hkl_pack_io io{};
   for (int k = 0; k < n_nets; ++k) io.net[k] = nets[k];
   io.step = step;

@@ -63,14 +63,15 @@ class WgJob(ctypes.Structure):
 
 class Seg(ctypes.Structure):
     _fields_ = [("param", vp), ("m", vp), ("v", vp), ("src", vp), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
-                ("ld", ctypes.c_int64), ("chunks", ctypes.c_int32), ("stride", ctypes.c_int64)]
+                ("ld", ctypes.c_int64), ("chunks", ctypes.c_int32), ("stride", ctypes.c_int64), ("target", vp)]
 
 
 class AdamIO(ctypes.Structure):
     _fields_ = [("seg", Seg * MAX_SEG), ("n_seg", ctypes.c_int32), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
                 ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("wd", ctypes.c_float), ("step", vp),
                 ("loss_src", vp), ("loss_chunks", ctypes.c_int32), ("loss_scale", ctypes.c_float),
-                ("loss_sum", vp), ("loss_count", vp)]
+                ("loss_sum", vp), ("loss_count", vp), ("polyak", ctypes.c_int32), ("polyak_rho", ctypes.c_float),
+                ("polyak_tau", ctypes.c_float)]
 
 
 EXPORTS = ["hkl_last_error", "hkl_pack_floats", "hkl_pack", "hkl_critic_step", "hkl_actor_step", "hkl_wgrad",
@@ -248,26 +249,32 @@ class FusedLearner:
         G, C, C1 = self.B // 64, self.B // (512 if self.B % 512 == 0 else 256), self.B // 256
         # Adam segments: torch parameter order of each network (fc1.w, fc1.b, fc2.w, fc2.b, fc3.w, fc3.b)
         self.adam = {}
-        for name, nets, lr, wd in (("critic", [("q1", 0), ("q2", 1)], self.cfg.lr_q, self.cfg.wd_q),
-                                   ("actor", [("actor", None)], self.cfg.lr_pol, self.cfg.wd_pol)):
+        for name, nets, lr, wd, tau in (
+                ("critic", [("q1", 0, "tq1"), ("q2", 1, "tq2")], self.cfg.lr_q, self.cfg.wd_q, self.cfg.tau_critic),
+                ("actor", [("actor", None, "target_actor")], self.cfg.lr_pol, self.cfg.wd_pol, self.cfg.tau_actor)):
             io = AdamIO()
             segs = []
             flat, m, v = self.flat[name], self.m[name], self.v[name]
+            tflat = self.flat["target_" + name]
             off = 0
-            for key, k in nets:
+            for key, k, tkey in nets:
                 f1, f2, f3 = _mlp_layers(n[key].m)
+                t1, t2, t3 = _mlp_layers(n[tkey].m)
+                tparams = (t1.weight, t1.bias, t2.weight, t2.bias, t3.weight, t3.bias)
                 if k is None:
                     srcs = [(b["sa_w1"], XP, C1, 256 * XP), (b["sa_b1"], 256, C1, 256), (b["sa_w2"], 256, C, 65536),
                             (b["sa_b2"], 256, C, 256), (b["pa_dw3"], 256, G, 1024), (b["pa_db3"], 4, G, 4)]
                 else:
                     srcs = [(b["s_w1"][k], XP, C1, 256 * XP), (b["s_b1"][k], 256, C1, 256), (b["s_w2"][k], 256, C, 65536),
                             (b["s_b2"][k], 256, C, 256), (b["p_dw3"][k], 256, G, 256), (b["p_db3"][k], 1, G, 1)]
-                for p, (src, ld, chunks, stride) in zip((f1.weight, f1.bias, f2.weight, f2.bias, f3.weight, f3.bias),
-                                                        srcs):
+                for p, tp, (src, ld, chunks, stride) in zip((f1.weight, f1.bias, f2.weight, f2.bias, f3.weight,
+                                                             f3.bias), tparams, srcs):
                     rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.shape[0])
                     assert p.data_ptr() == flat.data_ptr() + off * 4, "parameters not in the flat buffer's order"
+                    assert tp.data_ptr() == tflat.data_ptr() + off * 4 and tp.shape == p.shape, "target layout differs"
                     segs.append(Seg(_p(p), ctypes.c_void_p(m.data_ptr() + off * 4),
-                                    ctypes.c_void_p(v.data_ptr() + off * 4), _p(src), rows, cols, ld, chunks, stride))
+                                    ctypes.c_void_p(v.data_ptr() + off * 4), _p(src), rows, cols, ld, chunks, stride,
+                                    _p(tp)))
                     off += p.numel()
             assert off == flat.numel()
             for i, s in enumerate(segs):
@@ -278,6 +285,8 @@ class FusedLearner:
             io.loss_src = _p(b["loss_c"] if name == "critic" else b["loss_a"])
             io.loss_chunks = G
             io.loss_scale = (0.5 if name == "critic" else 1.0) / self.B
+            # soft_update folded into the Adam launch (set per call: the critic's only on actor updates)
+            io.polyak, io.polyak_rho, io.polyak_tau = 0, 1.0 - tau, tau
             self.adam[name] = io
         # weight-gradient jobs (one launch per k width): critics' dW2 / dW1 (+ b2 / b1), actor's
         J = lambda dz, x, sl, bs: WgJob(_p(dz), _p(x), _p(sl), _p(bs))  # noqa: E731
@@ -326,6 +335,9 @@ class FusedLearner:
             self.iw.copy_(iw / iw.max())
         _check(L.hkl_critic_step(ctypes.byref(self.cio), st), "hkl_critic_step")
         _check(L.hkl_wgrad_pair(self.wg["c256"], 2, self.wg["c32"], 2, self.B, st), "hkl_wgrad_pair")
+        # on an actor update the critic's soft_update runs here, with its Adam step: nothing later in the update
+        # reads the target critic or changes the critic, so the values are those of soft_update at the end
+        self.adam["critic"].polyak = 1 if train_actor else 0
         _check(L.hkl_adam(ctypes.byref(self.adam["critic"]), st), "hkl_adam")
         self._pack([self.nets["q1"], self.nets["q2"]], self.step["critic"], st)
         if self.ring.prioritized:
@@ -335,14 +347,10 @@ class FusedLearner:
             return
         _check(L.hkl_actor_step(ctypes.byref(self.aio), st), "hkl_actor_step")
         _check(L.hkl_wgrad_pair(self.wg["a256"], 1, self.wg["a32"], 1, self.B, st), "hkl_wgrad_pair")
+        self.adam["actor"].polyak = 1  # the actor's soft_update with its Adam step
         _check(L.hkl_adam(ctypes.byref(self.adam["actor"]), st), "hkl_adam")
-        self._pack([self.nets["actor"]], self.step["actor"], st)
-        ta, tc = c.tau_actor, c.tau_critic
-        _check(L.hkl_polyak(_p(self.flat["target_actor"]), _p(self.flat["actor"]), self.flat["actor"].numel(),
-                            1.0 - ta, ta, st), "hkl_polyak")
-        _check(L.hkl_polyak(_p(self.flat["target_critic"]), _p(self.flat["critic"]), self.flat["critic"].numel(),
-                            1.0 - tc, tc, st), "hkl_polyak")
-        self._pack([self.nets["target_actor"], self.nets["tq1"], self.nets["tq2"]], None, st)
+        self._pack([self.nets["actor"], self.nets["target_actor"], self.nets["tq1"], self.nets["tq2"]],
+                   self.step["actor"], st)
 
 
 def update_flops(batch, h=256, n_obs=18, n_act=4, policy_freq=2):

@@ -63,7 +63,8 @@ typedef struct {
   float *p_loss;
 } hkl_actor_io;
 
-/* one parameter tensor for hkl_adam: grad[r][c] = sum_{k < chunks} src[k * stride + r * ld + c] */
+/* one parameter tensor for hkl_adam: grad[r][c] = sum_{k < chunks} src[k * stride + r * ld + c]; target
+ * (optional): the tensor's soft-update twin in the target network, updated when hkl_adam_io.polyak is set */
 typedef struct {
   float *param, *m, *v;
   const float *src;
@@ -71,6 +72,7 @@ typedef struct {
   int64_t ld;
   int32_t chunks;
   int64_t stride;
+  float *target;
 } hkl_seg;
 
 typedef struct {
@@ -82,16 +84,21 @@ typedef struct {
   int32_t loss_chunks;
   float loss_scale;
   double *loss_sum, *loss_count;
+  /* polyak != 0: after its Adam step every parameter p with a segment target t also takes soft_update
+   * (learner.py:214-218): t = t * polyak_rho + polyak_tau * p, each product rounded (torch's mul_ then add_) --
+   * the same values as hkl_polyak after hkl_adam, one launch fewer */
+  int32_t polyak;
+  float polyak_rho, polyak_tau;
 } hkl_adam_io;
 
 typedef struct {
-  hkl_net net[3];
+  hkl_net net[4];
   int64_t *step;
 } hkl_pack_io;
 
 const char *hkl_last_error(void);
 int hkl_pack_floats(void);
-/* re-lay the weights of 1..3 networks out as MFMA operands; advances *step by one when step != NULL */
+/* re-lay the weights of 1..4 networks out as MFMA operands; advances *step by one when step != NULL */
 int hkl_pack(const hkl_net *nets, int n_nets, int64_t *step, void *stream);
 int hkl_critic_step(const hkl_critic_io *io, void *stream);
 int hkl_actor_step(const hkl_actor_io *io, void *stream);

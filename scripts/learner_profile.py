@@ -9,7 +9,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "hockey-env_amd"))
+sys.path.insert(0, os.environ.get("HK_PKG_DIR") or os.path.join(ROOT, "hockey-env_amd"))  # HK_PKG_DIR: an A/B copy
 import torch  # noqa: E402
 
 from hockey_amd.td3 import TD3, Learner, ReplayRing, TD3Config  # noqa: E402

@@ -8,6 +8,7 @@
 Tolerances: fp32 with a different summation order (MFMA fma chains vs the reference's BLAS): losses within
 1e-4 relative, parameters within 1e-5 absolute after the sequence (Adam steps are ~lr = 4e-4 per update, so a
 wrong gradient sign or scale moves a parameter by ~1e-4 per update and fails)."""
+import ctypes
 import os
 import sys
 
@@ -159,6 +160,36 @@ def test_fused_graph_replay_equals_fused_eager():
                                list(agent.critic.parameters()) + list(agent.target_actor.parameters()) +
                                list(agent.target_critic.parameters())]))
     assert torch.equal(nets[0], nets[1]), (nets[0] - nets[1]).abs().max()
+
+
+def test_packs_current_after_updates_with_folded_soft_update():
+    """soft_update runs inside the Adam launches (the critic's on actor updates only) and the actor and target
+    packs are re-laid in one launch: after critic-only and actor updates every network's operand pack is
+    bit-identical to what hkl_pack writes from its weights now, and each optimiser's step count advanced once per
+    Adam step."""
+    from hockey_amd import learner_hip as LH
+
+    torch.manual_seed(5)
+    cfg = TD3Config()
+    agent = TD3(cfg, device=DEV, seed=5)
+    cap = 8192
+    ring = ReplayRing(cap, device=DEV)
+    ring.push(torch.randn(cap, 18, device=DEV), torch.rand(cap, 4, device=DEV) * 2 - 1, torch.randn(cap, device=DEV),
+              torch.randn(cap, 18, device=DEV), (torch.rand(cap, device=DEV) < 0.1).float())
+    lr = Learner(agent, ring, 2048, graphs=False, fused=True)
+    f = lr.fused
+    for k in range(5):
+        f.update(train_actor=k % 2 == 1)
+    torch.cuda.synchronize()
+    assert int(f.step["critic"]) == 5 and int(f.step["actor"]) == 2
+    st = ctypes.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    for key, nb in f.nets.items():
+        fresh = torch.full_like(nb.pack, float("nan"))
+        net = LH.Net.from_buffer_copy(nb.net)
+        net.pack = fresh.data_ptr()
+        LH._check(LH.lib().hkl_pack((LH.Net * 1)(net), 1, None, st), "hkl_pack")
+        torch.cuda.synchronize()
+        assert torch.equal(nb.pack, fresh), (key, (nb.pack - fresh).abs().max())
 
 
 def test_fused_tanh_accuracy():
