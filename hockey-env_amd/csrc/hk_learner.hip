@@ -793,14 +793,21 @@ int hkl_actor_step(const hkl_actor_io *io, void *stream) {
   return e == hipSuccess ? HKL_OK : fail(e, "hkl_actor_step");
 }
 
+// samples per split-K chunk (include/hockey_learner.h hkl_wgrad): a single k-width-256 job has 4 x B / 512 tiles
+// at 512, half the workgroups the chip holds at C5's batch, so it takes 256-sample chunks
+static int wg_chunk_size(int n_jobs, int k_width, int64_t batch) {
+  return (k_width == 256 && n_jobs >= 2 && batch % 512 == 0) ? 512 : 256;
+}
+
 int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch, void *stream) {
   if (!jobs || n_jobs < 1 || n_jobs > 4 || batch <= 0 || batch % CHUNK || (k_width != 256 && k_width != XP))
     return HKL_E_INVALID;
   WgJobs J{};
   for (int k = 0; k < n_jobs; ++k) J.job[k] = WgJob{jobs[k].dz, jobs[k].x, jobs[k].slab, jobs[k].bias_slab, k_width};
-  // dW2 (k width 256): 512-sample chunks when the batch allows (fewer partial slabs for adam to add); dW1 (k width
-  // 32, a small tile per block): 256, for more blocks
-  J.chunk_size = (k_width == 256 && batch % 512 == 0) ? 512 : 256;
+  // dW2 (k width 256): 512-sample chunks when the batch allows and two or more networks fill the chip (fewer
+  // partial slabs for adam to add); one network (the actor) or dW1 (k width 32, a small tile per block): 256, for
+  // more blocks
+  J.chunk_size = wg_chunk_size(n_jobs, k_width, batch);
   J.chunks = (int)(batch / J.chunk_size);
   const unsigned z = (unsigned)(J.chunks * n_jobs);
   if (k_width == 256) hipLaunchKernelGGL(wgrad_kernel<128>, dim3(2, 2, z), dim3(WG), 0, (hipStream_t)stream, J);
@@ -812,7 +819,7 @@ int hkl_wgrad(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch,
 static WgJobs wg_jobs(const hkl_wgrad_job *jobs, int n_jobs, int k_width, int64_t batch) {
   WgJobs J{};
   for (int k = 0; k < n_jobs; ++k) J.job[k] = WgJob{jobs[k].dz, jobs[k].x, jobs[k].slab, jobs[k].bias_slab, k_width};
-  J.chunk_size = (k_width == 256 && batch % 512 == 0) ? 512 : 256;
+  J.chunk_size = wg_chunk_size(n_jobs, k_width, batch);
   J.chunks = (int)(batch / J.chunk_size);
   return J;
 }

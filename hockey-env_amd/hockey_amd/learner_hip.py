@@ -170,7 +170,8 @@ class FusedLearner:
         if agent.actor.fc1.out_features != 256:
             raise ValueError("fused learner: hidden width 256 only (rl/td3/networks.py h)")
         B, G = self.B, self.B // 64
-        C = self.B // (512 if self.B % 512 == 0 else 256)  # hkl_wgrad's split-K chunks: dW2 (k width 256)
+        C = self.B // (512 if self.B % 512 == 0 else 256)  # hkl_wgrad's split-K chunks: the critics' dW2 (2 jobs)
+        CA = self.B // 256  # the actor's dW2 (one k-width-256 job: 256-sample chunks, include/hockey_learner.h)
         C1 = self.B // 256  # dW1 (k width 32)
         c = agent.cfg
         self.cfg = c
@@ -195,8 +196,8 @@ class FusedLearner:
         self.buf["s_w2"] = [z(C, 256, 256), z(C, 256, 256)]
         self.buf["s_w1"] = [z(C1, 256, XP), z(C1, 256, XP)]
         self.buf["s_b2"], self.buf["s_b1"] = [z(C, 256), z(C, 256)], [z(C1, 256), z(C1, 256)]
-        self.buf["sa_w2"], self.buf["sa_w1"] = z(C, 256, 256), z(C1, 256, XP)
-        self.buf["sa_b2"], self.buf["sa_b1"] = z(C, 256), z(C1, 256)
+        self.buf["sa_w2"], self.buf["sa_w1"] = z(CA, 256, 256), z(C1, 256, XP)
+        self.buf["sa_b2"], self.buf["sa_b1"] = z(CA, 256), z(C1, 256)
         self.idx = torch.zeros(B, dtype=torch.int64, device=dev)
         self.sample_counter = torch.zeros((), dtype=torch.int64, device=dev)
         sio = SampleIO()
@@ -247,6 +248,7 @@ class FusedLearner:
         aio.p_loss = _p(b["loss_a"])
         self.aio = aio
         G, C, C1 = self.B // 64, self.B // (512 if self.B % 512 == 0 else 256), self.B // 256
+        CA = self.B // 256
         # Adam segments: torch parameter order of each network (fc1.w, fc1.b, fc2.w, fc2.b, fc3.w, fc3.b)
         self.adam = {}
         for name, nets, lr, wd, tau in (
@@ -262,8 +264,8 @@ class FusedLearner:
                 t1, t2, t3 = _mlp_layers(n[tkey].m)
                 tparams = (t1.weight, t1.bias, t2.weight, t2.bias, t3.weight, t3.bias)
                 if k is None:
-                    srcs = [(b["sa_w1"], XP, C1, 256 * XP), (b["sa_b1"], 256, C1, 256), (b["sa_w2"], 256, C, 65536),
-                            (b["sa_b2"], 256, C, 256), (b["pa_dw3"], 256, G, 1024), (b["pa_db3"], 4, G, 4)]
+                    srcs = [(b["sa_w1"], XP, C1, 256 * XP), (b["sa_b1"], 256, C1, 256), (b["sa_w2"], 256, CA, 65536),
+                            (b["sa_b2"], 256, CA, 256), (b["pa_dw3"], 256, G, 1024), (b["pa_db3"], 4, G, 4)]
                 else:
                     srcs = [(b["s_w1"][k], XP, C1, 256 * XP), (b["s_b1"][k], 256, C1, 256), (b["s_w2"][k], 256, C, 65536),
                             (b["s_b2"][k], 256, C, 256), (b["p_dw3"][k], 256, G, 256), (b["p_db3"][k], 1, G, 1)]

@@ -103,7 +103,8 @@ int hkl_pack(const hkl_net *nets, int n_nets, int64_t *step, void *stream);
 int hkl_critic_step(const hkl_critic_io *io, void *stream);
 int hkl_actor_step(const hkl_actor_io *io, void *stream);
 /* weight-gradient job: slab[c][256][k_width] = sum over the samples j of chunk c (k_width 256: 512 samples each
- * when the batch is a multiple of 512, else 256; k_width 32: 256) of dz[j][o] x[j][k]
+ * when the launch has two or more k-width-256 jobs and the batch is a multiple of 512, else 256; k_width 32: 256)
+ * of dz[j][o] x[j][k]
  * (dz [B][256], x [B][k_width]); bias_slab (optional) [c][256] = the chunk's column sums of dz */
 typedef struct {
   const float *dz, *x;

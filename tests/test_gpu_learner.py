@@ -268,3 +268,13 @@ def test_wgrad_pair_equals_two_wgrad_launches():
     # and they are the weight gradients: chunk sums of DZ^T X
     ref = dz2[0].double().T @ h1[0].double()
     assert torch.allclose(outs[1][0].double().sum(0), ref, rtol=1e-4, atol=1e-3)
+    # one k-width-256 job (the actor's) takes 256-sample chunks: B / 256 slabs, the same sums
+    s2a, b2a = torch.full((B // 256, H, H), 7.0, device=DEV), torch.full((B // 256, H), 7.0, device=DEV)
+    s1a, b1a = torch.full((C1, H, XP), 7.0, device=DEV), torch.full((C1, H), 7.0, device=DEV)
+    wide = (WgJob * 1)(WgJob(_p(dz2[0]), _p(h1[0]), _p(s2a), _p(b2a)))
+    narrow = (WgJob * 1)(WgJob(_p(dz1[0]), _p(x0), _p(s1a), _p(b1a)))
+    assert L.hkl_wgrad_pair(wide, 1, narrow, 1, B, st) == 0
+    torch.cuda.synchronize()
+    assert torch.allclose(s2a.double().sum(0), ref, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(b2a.double().sum(0), dz2[0].double().sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.equal(s1a, outs[1][4]) and torch.equal(b1a, outs[1][6])
