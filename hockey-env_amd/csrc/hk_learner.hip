@@ -281,6 +281,62 @@ __device__ __forceinline__ void input_frags(const float *__restrict__ srow, cons
   }
 }
 
+// ------------------------------------------------------------------------------------------------ sampling
+// The batch's replay slots and target noise from a counter-based RNG (Philox4x32-10 keyed by the learner's seed, the
+// counter = (sample, update, purpose)): uniform slots floor(u * size) with a 53-bit u (rl/replay/uniform_buffer.py's
+// (rand * size).astype(int)), and the target policy smoothing noise clamp(N(0, scale), -clip, clip) by Box-Muller
+// (learner.py:80-93).  The update counter lives in device memory (graph replays advance it): critic_step bumps it.
+struct P4 {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ P4 philox(uint64_t key, P4 c) {
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = P4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+// sample e's replay slot of update `ctr` over `size` filled slots
+__device__ __forceinline__ int64_t sample_slot(uint64_t seed, int64_t e, uint64_t ctr, uint64_t size) {
+  const P4 r0 = philox(seed, P4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32)});
+  const uint64_t bits = (((uint64_t)r0.x << 32) | r0.y) >> 11;
+  const double u = (double)bits * (1.0 / 9007199254740992.0);
+  const uint64_t i = (uint64_t)(u * (double)size);
+  return (int64_t)(i < size ? i : size - 1);
+}
+// sample e's clipped target-smoothing noise of update `ctr`
+__device__ __forceinline__ f4 sample_noise(uint64_t seed, int64_t e, uint64_t ctr, float scale, float clip) {
+  const P4 r1 = philox(seed ^ 0x6E6F697365ull, P4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32)});
+  const uint32_t w[4] = {r1.x, r1.y, r1.z, r1.w};
+  float z[4];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float u1 = ((float)(w[2 * p] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+    const float u2 = (float)(w[2 * p + 1] >> 8) * (1.0f / 16777216.0f);
+    const float rad = sqrtf(-2.0f * logf(u1));
+    float sn, cs;
+    sincosf(6.283185307179586f * u2, &sn, &cs);
+    z[2 * p] = rad * cs;
+    z[2 * p + 1] = rad * sn;
+  }
+  f4 nz;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) nz[c] = fminf(fmaxf(z[c] * scale, -clip), clip);
+  return nz;
+}
+__global__ void __launch_bounds__(256) sample_kernel(hkl_sample_io io) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= io.batch) return;
+  const uint64_t ctr = (uint64_t)*io.counter, size = (uint64_t)*io.size;
+  io.idx[e] = sample_slot(io.seed, e, ctr, size);
+  *reinterpret_cast<f4 *>(io.noise + e * 4) = sample_noise(io.seed, e, ctr, io.scale, io.clip);
+}
+
 // ------------------------------------------------------------------------------------------------ critic step
 // Q(x) of one critic network (forward only): its output for this lane's sample
 __device__ __forceinline__ float q_forward(const Net &c, const float (&x)[S1], Tile &h1, Tile &h2, int lane,
@@ -668,54 +724,6 @@ __global__ void __launch_bounds__(256) polyak_kernel(float *__restrict__ t, cons
   if (e < n) t[e] = t[e] * rho + tau * p[e];
 }
 
-// ------------------------------------------------------------------------------------------------ sampling
-// The batch's replay slots and target noise from a counter-based RNG (Philox4x32-10 keyed by the learner's seed, the
-// counter = (sample, update, purpose)): uniform slots floor(u * size) with a 53-bit u (rl/replay/uniform_buffer.py's
-// (rand * size).astype(int)), and the target policy smoothing noise clamp(N(0, scale), -clip, clip) by Box-Muller
-// (learner.py:80-93).  The update counter lives in device memory (graph replays advance it): critic_step bumps it.
-struct P4 {
-  uint32_t x, y, z, w;
-};
-__device__ __forceinline__ P4 philox(uint64_t key, P4 c) {
-  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-    c = P4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c;
-}
-__global__ void __launch_bounds__(256) sample_kernel(hkl_sample_io io) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= io.batch) return;
-  const uint64_t ctr = (uint64_t)*io.counter, size = (uint64_t)*io.size;
-  const P4 r0 = philox(io.seed, P4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32)});
-  const uint64_t bits = (((uint64_t)r0.x << 32) | r0.y) >> 11;
-  const double u = (double)bits * (1.0 / 9007199254740992.0);
-  const uint64_t i = (uint64_t)(u * (double)size);
-  io.idx[e] = (int64_t)(i < size ? i : size - 1);
-  const P4 r1 = philox(io.seed ^ 0x6E6F697365ull, P4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32)});
-  const uint32_t w[4] = {r1.x, r1.y, r1.z, r1.w};
-  float z[4];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const float u1 = ((float)(w[2 * p] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
-    const float u2 = (float)(w[2 * p + 1] >> 8) * (1.0f / 16777216.0f);
-    const float rad = sqrtf(-2.0f * logf(u1));
-    float sn, cs;
-    sincosf(6.283185307179586f * u2, &sn, &cs);
-    z[2 * p] = rad * cs;
-    z[2 * p + 1] = rad * sn;
-  }
-  f4 nz;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) nz[c] = fminf(fmaxf(z[c] * io.scale, -io.clip), io.clip);
-  *reinterpret_cast<f4 *>(io.noise + e * 4) = nz;
-}
-
 __global__ void tanh_probe_kernel(const float *x, float *y, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e < n) y[e] = tanh_fast(x[e]);
@@ -837,6 +845,10 @@ int hkl_wgrad_pair(const hkl_wgrad_job *wide, int n_wide, const hkl_wgrad_job *n
 
 int hkl_adam(const hkl_adam_io *io, void *stream) {
   if (!io || io->n_seg < 1 || io->n_seg > HKL_MAX_SEG) return HKL_E_INVALID;
+  if (io->loss_src && (!io->loss_sum || !io->loss_count)) return HKL_E_INVALID;  // loss partials need a destination
+  for (int s = 0; s < io->n_seg; ++s)
+    if (!io->seg[s].param || !io->seg[s].m || !io->seg[s].v || !io->seg[s].src || (io->polyak && !io->seg[s].target))
+      return HKL_E_INVALID;
   int64_t n = 0;
   for (int s = 0; s < io->n_seg; ++s) n += (int64_t)io->seg[s].rows * io->seg[s].cols;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *io);

@@ -211,6 +211,9 @@ class FusedLearner:
         low = agent.critic.action_low.float().cpu().tolist()
         rng = agent.critic.action_range.float().cpu().tolist()
         self._build_io(low, rng)
+        # Adam adds each step's loss into a device accumulator: a private one until the caller sets its own, so
+        # that an update never runs with the loss pointers unset
+        self.set_loss_accumulator(torch.zeros(4, dtype=torch.float64, device=dev))
         st = self._stream()
         for group in (("actor", "target_actor"), ("q1", "q2"), ("tq1", "tq2")):
             self._pack([self.nets[k] for k in group], None, st)
@@ -237,6 +240,7 @@ class FusedLearner:
         cio.p_loss, cio.td = _p(b["loss_c"]), _p(b["td"])
         cio.sample_counter = _p(self.sample_counter)
         self.cio = cio
+
         aio = ActorIO()
         aio.batch, aio.idx, aio.ring_s = self.B, _p(self.idx), _p(r.s)
         aio.actor, aio.q1 = n["actor"].net, n["q1"].net

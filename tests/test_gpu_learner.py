@@ -192,6 +192,23 @@ def test_packs_current_after_updates_with_folded_soft_update():
         assert torch.equal(nb.pack, fresh), (key, (nb.pack - fresh).abs().max())
 
 
+def test_fused_learner_runs_without_a_caller_accumulator():
+    """FusedLearner used directly (no set_loss_accumulator call) still has a device accumulator for the Adam
+    launches' loss sums: two updates run, and its counts read one critic and one actor step per actor update."""
+    from hockey_amd.learner_hip import FusedLearner
+
+    cap = 4096
+    ring = ReplayRing(cap, device=DEV)
+    ring.push(torch.randn(cap, 18, device=DEV), torch.rand(cap, 4, device=DEV) * 2 - 1, torch.randn(cap, device=DEV),
+              torch.randn(cap, 18, device=DEV), torch.zeros(cap, device=DEV))
+    fl = FusedLearner(TD3(TD3Config(), device=DEV, seed=2), ring, 1024)
+    fl.update(train_actor=False)
+    fl.update(train_actor=True)
+    torch.cuda.synchronize()
+    acc = fl._acc.cpu().tolist()
+    assert acc[2] == 2.0 and acc[3] == 1.0, acc
+
+
 def test_fused_tanh_accuracy():
     """The fused kernels' branch-free tanh against torch.tanh over [-20, 20] and near 0: |error| < 2e-7."""
     from hockey_amd.learner_hip import tanh_probe

@@ -180,3 +180,25 @@ def test_learner_ctypes_struct_layout_matches_header(tmp_path):
         assert ctypes.sizeof(S) == int(want[cname]), cname
         for f, _ in S._fields_:
             assert getattr(S, f).offset == int(want[f"{cname}.{f}"]), (cname, f)
+
+
+def test_learner_adam_rejects_incomplete_io_before_any_launch():
+    """hkl_adam validates its pointers on the host (no GPU needed): loss partials without a destination, or a folded
+    soft update without target twins, return HKL_E_INVALID instead of launching a kernel that would write through a
+    null pointer."""
+    from hockey_amd import learner_hip as LH
+
+    L = LH.lib()
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    io = LH.AdamIO()
+    io.seg[0] = LH.Seg(p, p, p, p, 1, 8, 8, 1, 8, p)
+    io.n_seg = 1
+    io.loss_src = p  # loss partials, but no loss_sum / loss_count
+    assert L.hkl_adam(ctypes.byref(io), None) == 1
+    io.loss_src = None
+    io.polyak = 1
+    io.seg[0].target = None  # soft update asked, no target twin
+    assert L.hkl_adam(ctypes.byref(io), None) == 1
+    io.n_seg = 0
+    assert L.hkl_adam(ctypes.byref(io), None) == 1
