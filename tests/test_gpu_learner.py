@@ -295,3 +295,53 @@ def test_wgrad_pair_equals_two_wgrad_launches():
     assert torch.allclose(s2a.double().sum(0), ref, rtol=1e-4, atol=1e-3)
     assert torch.allclose(b2a.double().sum(0), dz2[0].double().sum(0), rtol=1e-4, atol=1e-3)
     assert torch.equal(s1a, outs[1][4]) and torch.equal(b1a, outs[1][6])
+
+
+def _pack_reference(w1, w2, w3, n_in, n_out):
+    """numpy restatement of hk_learner.hip's operand pack (f1, fp, bp, fo, wa) from torch Linear weights."""
+    H = 256
+    f1 = np.zeros((16, 64, 8), np.float32)
+    fp = np.zeros((16, 16, 64, 4), np.float32)
+    bp = np.zeros((16, 16, 64, 4), np.float32)
+    fo = np.zeros((16, 64, 4), np.float32)
+    wa = np.zeros((256, 4), np.float32)
+    lane = np.arange(64)
+    lo, hi = lane & 15, lane >> 4
+    for ob in range(16):
+        for s in range(6):
+            c = 4 * s + hi
+            ok = c < n_in
+            f1[ob, ok, s] = w1[16 * ob + lo[ok], c[ok]]
+        for kb in range(16):
+            for r in range(4):
+                fp[ob, kb, :, r] = w2[16 * ob + lo, 16 * kb + 4 * hi + r]
+                bp[kb, ob, :, r] = w2[16 * ob + 4 * hi + r, 16 * kb + lo]
+    for kb in range(16):
+        for r in range(4):
+            ok = lo < n_out
+            fo[kb, ok, r] = w3[lo[ok], 16 * kb + 4 * hi[ok] + r]
+    if n_in == 22:
+        wa[:, :] = w1[:, 18:22]
+    assert fp.size == bp.size == 16 * 16 * 64 * 4 and H == 256
+    return np.concatenate([f1.ravel(), fp.ravel(), bp.ravel(), fo.ravel(), wa.ravel()])
+
+
+def test_operand_pack_layout_matches_numpy_restatement():
+    """hkl_pack's MFMA operand layouts (f1 / fp / bp / fo / wa, hk_learner.hip) against an independent numpy
+    restatement, for an actor (18 -> 256 -> 256 -> 4) and a critic (22 -> 256 -> 256 -> 1)."""
+    from hockey_amd.learner_hip import FusedLearner, PACK_FLOATS
+
+    cap = 1024
+    ring = ReplayRing(cap, device=DEV)
+    ring.push(torch.randn(cap, 18, device=DEV), torch.rand(cap, 4, device=DEV) * 2 - 1, torch.randn(cap, device=DEV),
+              torch.randn(cap, 18, device=DEV), torch.zeros(cap, device=DEV))
+    fl = FusedLearner(TD3(TD3Config(), device=DEV, seed=9), ring, 256)
+    torch.cuda.synchronize()
+    for key in ("actor", "q1"):
+        nb = fl.nets[key]
+        f1, f2, f3 = nb.m.fc1, nb.m.fc2, nb.m.fc3
+        ref = _pack_reference(f1.weight.detach().cpu().numpy(), f2.weight.detach().cpu().numpy(),
+                              f3.weight.detach().cpu().numpy(), f1.in_features, f3.out_features)
+        assert ref.size == PACK_FLOATS
+        got = nb.pack.cpu().numpy()
+        assert np.array_equal(got, ref), (key, int(np.argmax(got != ref)))
