@@ -193,6 +193,30 @@ __device__ __forceinline__ f4 gemm_out(const f4 *__restrict__ fo, Tile &h, const
   return o;
 }
 
+// A one-output head (a critic's Q): W3[0] . tanh(h + bias) + b3[0] for this lane's sample, returned to every lane of
+// the sample, h activated in place as gemm_out leaves it.  VALU dot products (each lane's 64 neurons, four partial
+// sums) and two cross-row shuffles instead of a 16 x 16 MFMA tile of which one row is used; no LDS staging and no
+// workgroup barrier.  The 4 lanes of a sample add the same partials in commuted order, so they agree bit for bit.
+__device__ __forceinline__ float head1(const float *__restrict__ w3, Tile &h, const float *__restrict__ bias,
+                                       const float *__restrict__ b3, int lane) {
+  const int q = lane >> 4;
+  f4 acc = z4();
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) {
+    const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * ob + 4 * q);
+    const f4 w = *reinterpret_cast<const f4 *>(w3 + 16 * ob + 4 * q);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      h.v[ob][r] = tanh_fast(h.v[ob][r] + bb[r]);
+      acc[r] += w[r] * h.v[ob][r];
+    }
+  }
+  float v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v + b3[0];
+}
+
 // dh = W3^T dz3 (dz3: this lane's sample's n_out output gradients)
 __device__ __forceinline__ void back_out(const float *__restrict__ w3, int n_out, f4 dz3, Tile &dh, int q) {
 #pragma unroll
@@ -343,7 +367,7 @@ __device__ __forceinline__ float q_forward(const Net &c, const float (&x)[S1], T
                                            f4 *sfrag) {
   gemm_in(c.f1(), x, h1, lane, sfrag);
   gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
-  return gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane, sfrag)[0];
+  return head1(c.w3, h2, c.b2, c.b3, lane);
 }
 
 // one critic k of update_critic: forward on x, the weighted smooth-L1 (torch_utils.py:12-24; critic_loss =
@@ -356,7 +380,7 @@ __device__ __forceinline__ void critic_one(const hkl_critic_io &io, int k, const
   gemm_in(c.f1(), x, h1, lane, sfrag);
   gemm256(c.fp(), h1, c.b1, h2, lane, sfrag);
   store_tile(io.h1[k], h1, row, q);
-  const float qv = gemm_out(c.fo(), h2, c.b2, c.b3, 1, lane, sfrag)[0];
+  const float qv = head1(c.w3, h2, c.b2, c.b3, lane);
   const float diff = qv - y, ad = fabsf(diff);
   loss += ad < 1.0f ? 0.5f * w * diff * diff : (ad - 0.5f) * w;
   const float g = (ad < 1.0f ? w * diff : (diff > 0.0f ? w : diff < 0.0f ? -w : 0.0f)) * (0.5f / (float)io.batch);
@@ -468,7 +492,7 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   input_frags(s_row, au, true, x, q);
   gemm_in(qn.f1(), x, h1, lane, sfrag);
   gemm256(qn.fp(), h1, qn.b1, h2, lane, sfrag);
-  const float qv = gemm_out(qn.fo(), h2, qn.b2, qn.b3, 1, lane, sfrag)[0];
+  const float qv = head1(qn.w3, h2, qn.b2, qn.b3, lane);
   const float g = -1.0f / (float)io.batch;  // d(-mean q) / dq
   Tile t;
   back_out(qn.w3, 1, f4{g, 0.0f, 0.0f, 0.0f}, t, q);
