@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(WG, 1) actor_step_kernel(hkl_actor_io io) {
   input_frags(s_row, au, true, x, q);
   gemm_in(qn.f1(), x, h1, lane, sfrag);
   gemm256(qn.fp(), h1, qn.b1, h2, lane, sfrag);
-  const float qv = head1(qn.w3, h2, qn.b2, qn.b3, lane);
+  const float qv = gemm_out(qn.fo(), h2, qn.b2, qn.b3, 1, lane, sfrag)[0];
   const float g = -1.0f / (float)io.batch;  // d(-mean q) / dq
   Tile t;
   back_out(qn.w3, 1, f4{g, 0.0f, 0.0f, 0.0f}, t, q);
