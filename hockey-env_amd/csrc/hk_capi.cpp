@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/hockey.h"
@@ -46,19 +47,38 @@ struct Ctx {
   int hs_staged = 0;
   uint64_t hs_seq = 0;  // hk_step_host steps so far (the completion word's expected value)
   // hk_step_host's resident server (mapped variant; HK_STEP_HOST_SERVER=0 launches one step kernel per call
-  // instead): it runs on a private stream, ordered after the caller's stream when it starts, and every other
-  // entry point stops it first (server_stop), so it never runs beside another kernel of this context.
+  // instead): it runs on the device's shared server stream (SrvSlot), ordered after the caller's stream when it
+  // starts, and every other entry point stops it first (server_stop), so it never runs beside another kernel of
+  // this context.
   int srv_on = 0;
-  hipStream_t srv_stream = nullptr;
   hipEvent_t srv_after = nullptr;
-  bool srv_running = false;
+  bool srv_running = false;  // guarded by the device's SrvSlot::mu
   std::chrono::steady_clock::time_point srv_start, srv_last;
   unsigned long long srv_idle_ticks = 0, srv_life_ticks = 0;
 };
 
 // the server's own limits (hk_kernels.h HostServer): it exits after kSrvIdleMs without a request or kSrvLifeMs in
-// all; the host replaces it before either can fire mid-request (half those times), and relaunches on demand
-constexpr int kSrvIdleMs = 20, kSrvLifeMs = 2000;
+// all; the host replaces it before either can fire mid-request (half those times), and relaunches on demand.  The
+// idle limit bounds what a resident server can cost other work: a kernel that lands on the server stream's hardware
+// queue (streams share the box's 4 queues) or a device-wide synchronise waits for its idle exit.
+constexpr int kSrvIdleMs = 4, kSrvLifeMs = 2000;
+
+// At most ONE resident step server per device and process: every single-arena context's server runs on
+// the device's one server stream, and a context that starts its server first stops the running one of another
+// context.  So N facades stepped round-robin cost a server hand-over per step (a quit, a stream sync and a launch:
+// tens of microseconds), never a kernel queued behind another context's idle server.  ``mu`` is held for a whole
+// server-path hk_step_host call and by server_stop, so a hand-over never interrupts a request in flight on another
+// thread.
+struct SrvSlot {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  Ctx *owner = nullptr;
+};
+constexpr int kMaxDevices = 64;
+SrvSlot &srv_slot(int device) {
+  static SrvSlot slots[kMaxDevices];
+  return slots[device];
+}
 
 // hk_step_host buffer layout per context: inputs [N,8] f32 actions + [N,2] f64 increments, outputs [N] packed
 // records of HK_HOST_RECORD_BYTES (obs f32[18], obs2 f32[18], done u8 + 7 pad, record f64[16])
@@ -76,15 +96,22 @@ size_t host_pin_bytes(int64_t n) { return host_word_off(n) + 3 * kHostWordBytes;
 volatile uint64_t *req_word(Ctx *c) { return reinterpret_cast<volatile uint64_t *>(c->hs_pin + host_req_off(c->s.n)); }
 
 // stop hk_step_host's server (if one runs) and wait for it: every request it was given has been answered (a step
-// returns only then), so the next server starts idle
-hipError_t server_stop(Ctx *c) {
+// returns only then), so the next server starts idle.  The caller holds srv_slot(c->device).mu.
+hipError_t server_stop_locked(Ctx *c) {
+  SrvSlot &slot = srv_slot(c->device);
+  if (slot.owner == c) slot.owner = nullptr;
   if (!c->srv_running) return hipSuccess;
   std::atomic_thread_fence(std::memory_order_release);
   *req_word(c) = hk::kServerQuit;
-  const hipError_t e = hipStreamSynchronize(c->srv_stream);
+  const hipError_t e = hipStreamSynchronize(slot.stream);
   *req_word(c) = c->hs_seq;
   c->srv_running = false;
   return e;
+}
+hipError_t server_stop(Ctx *c) {
+  if (!c->srv_on) return hipSuccess;  // this context never started a server (srv_on is set by its own thread)
+  std::lock_guard<std::mutex> lk(srv_slot(c->device).mu);
+  return server_stop_locked(c);
 }
 #define HK_QUIESCE(c, who)                                               \
   do {                                                                   \
@@ -127,7 +154,8 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0) return fail(HK_E_DEVICE, "hk_create: no HIP device available%s");
-  if (device < 0 || device >= ndev) return fail(HK_E_DEVICE, "hk_create: device %s%lld out of range", "", device);
+  if (device < 0 || device >= ndev || device >= kMaxDevices)
+    return fail(HK_E_DEVICE, "hk_create: device %s%lld out of range", "", device);
   hipDeviceProp_t prop;
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return hipfail(e, "hipGetDeviceProperties");
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
@@ -176,8 +204,7 @@ int hk_destroy(void *ctx) {
   if (!ctx) return HK_OK;
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
-  (void)server_stop(c);
-  if (c->srv_stream) (void)hipStreamDestroy(c->srv_stream);
+  (void)server_stop(c);  // the shared server stream stays for the process's other contexts
   if (c->srv_after) (void)hipEventDestroy(c->srv_after);
   if (c->s.f) (void)hipFree(c->s.f);
   if (c->s.i) (void)hipFree(c->s.i);
@@ -279,13 +306,16 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
     c->hs_seq = 0;
     if (c->srv_on) {
       int khz = 0;
-      if ((e = hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking)) != hipSuccess ||
-          (e = hipEventCreateWithFlags(&c->srv_after, hipEventDisableTiming)) != hipSuccess ||
+      SrvSlot &slot = srv_slot(c->device);
+      {
+        std::lock_guard<std::mutex> lk(slot.mu);
+        if (!slot.stream && hipStreamCreateWithFlags(&slot.stream, hipStreamNonBlocking) != hipSuccess)
+          slot.stream = nullptr;
+      }
+      if (!slot.stream || (e = hipEventCreateWithFlags(&c->srv_after, hipEventDisableTiming)) != hipSuccess ||
           (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device)) != hipSuccess || khz <= 0) {
         // no server for this context: its steps take the launch-per-step path (still the GPU kernel)
-        if (c->srv_stream) (void)hipStreamDestroy(c->srv_stream);
         if (c->srv_after) (void)hipEventDestroy(c->srv_after);
-        c->srv_stream = nullptr;
         c->srv_after = nullptr;
         c->srv_on = 0;
       }
@@ -296,12 +326,17 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
   const hipStream_t st = (hipStream_t)stream;
   const size_t a_b = (size_t)n * 8 * 4, inc_b = (size_t)n * 2 * 8;
   if (c->srv_on) {
+    SrvSlot &slot = srv_slot(c->device);
+    std::lock_guard<std::mutex> lk(slot.mu);
+    // one resident server per device: hand the slot over from another context's server first
+    if (slot.owner && slot.owner != c && (e = server_stop_locked(slot.owner)) != hipSuccess)
+      return hipfail(e, "hk_step_host: another context's step server");
     // A server that has idled or lived for half its limits may be about to exit on its own: replace it now
     // rather than post a request it could miss (a missed request is still served: see the wait below).
     const auto now = std::chrono::steady_clock::now();
-    if (c->srv_running && (now - c->srv_last > std::chrono::milliseconds(kSrvIdleMs / 2) ||
+    if (c->srv_running && (now - c->srv_last > std::chrono::microseconds(kSrvIdleMs * 500) ||
                            now - c->srv_start > std::chrono::milliseconds(kSrvLifeMs / 2))) {
-      if ((e = server_stop(c)) != hipSuccess) return hipfail(e, "hk_step_host: step server");
+      if ((e = server_stop_locked(c)) != hipSuccess) return hipfail(e, "hk_step_host: step server");
     }
     if (actions) std::memcpy(c->hs_pin, actions, a_b);
     if (opp_inc) std::memcpy(c->hs_pin + a_b, opp_inc, inc_b);
@@ -332,10 +367,11 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
         hs.idle_ticks = c->srv_idle_ticks;
         hs.life_ticks = c->srv_life_ticks;
         if ((e = hipEventRecord(c->srv_after, st)) != hipSuccess ||
-            (e = hipStreamWaitEvent(c->srv_stream, c->srv_after, 0)) != hipSuccess ||
-            (e = hk::launch_host_server(c->s, c->cfg, s, hs, c->srv_stream)) != hipSuccess)
+            (e = hipStreamWaitEvent(slot.stream, c->srv_after, 0)) != hipSuccess ||
+            (e = hk::launch_host_server(c->s, c->cfg, s, hs, slot.stream)) != hipSuccess)
           return hipfail(e, "hk_step_host: server launch");
         c->srv_running = true;
+        slot.owner = c;
         c->srv_start = std::chrono::steady_clock::now();
       }
       // Spin on the completion word; every 4096 polls ask the server's stream, so a server that faulted returns
@@ -343,14 +379,16 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
       uint32_t k = 1;
       for (; *word != seq; ++k) {
         if ((k & 4095u) == 0u) {
-          const hipError_t q = hipStreamQuery(c->srv_stream);
+          const hipError_t q = hipStreamQuery(slot.stream);
           if (q == hipErrorNotReady) continue;
           if (q != hipSuccess) {
             c->srv_running = false;
+            slot.owner = nullptr;
             return hipfail(q, "hk_step_host: step server");
           }
           if (*word == seq) break;
           c->srv_running = false;  // exited (idle / life limit) without this request: start another
+          slot.owner = nullptr;
           break;
         }
       }

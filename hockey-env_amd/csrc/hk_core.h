@@ -254,6 +254,21 @@ HK_DEV bool wave_any(bool p) { return __ballot(p) != 0ull; }
 HK_DEV bool wave_any(bool p) { return p; }
 #endif
 
+// A per-lane all-ones / all-zeros mask the compiler cannot see through.  `x & mask` then stays one v_and per word:
+// written as `if (!c) x = 0` (or a select), LLVM sinks the computation of x into a branch on c and the structurizer
+// wraps every use in exec-mask save / xor / restore plus moves (~10 issue slots per velocity iteration, the
+// static-body-A reset of the one- and two-contact loops; r05, -DHK_ASM_MARKS dump).
+HK_DEV uint32_t lane_mask(bool c) {
+  uint32_t m = c ? 0xffffffffu : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(m));
+#else
+  asm volatile("" : "+r"(m));
+#endif
+  return m;
+}
+HK_DEV float mask_f(float x, uint32_t m) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m); }
+
 // Analysis build only (-DHK_ASM_MARKS): labels in the device assembly around hot regions.
 #ifdef HK_ASM_MARKS
 #define HK_MARK(x) asm volatile(";HKMARK " #x)

@@ -523,8 +523,8 @@ static_assert(kVelIters % 4 == 0, "the snapshot period divides the iteration cou
 // returns in the general loop; the snapshot compares the same values the general loop compares.
 // kSA: no running lane has a dynamic body A, so A's velocity row is dropped (fslot_solve_velocity_p).
 template <bool kSA, int kP>
-HK_DEV void vone_chunk(FSlot &s, bool dynA, f2 &vA, float &wA, f2 &vB, float &wB, uint32_t (&sn)[10], int &it,
-                       int stop, int first, bool &active) {
+HK_DEV void vone_chunk(FSlot &s, bool dynA, uint32_t mA, f2 &vA, float &wA, f2 &vB, float &wB, uint32_t (&sn)[10],
+                       int &it, int stop, int first, bool &active) {
   if constexpr (kSA && kP == 1) HK_MARK(vone_begin_s1);
   else if constexpr (kSA && kP == 2) HK_MARK(vone_begin_s2);
   else if constexpr (kSA) HK_MARK(vone_begin_s0);
@@ -534,10 +534,9 @@ HK_DEV void vone_chunk(FSlot &s, bool dynA, f2 &vA, float &wA, f2 &vB, float &wB
   for (; it < stop && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (!dynA) {
-        vA = f2{0.0f, 0.0f};
-        wA = 0.0f;
-      }
+      // a static body A is +0 at every solve (mA = 0 clears it to +0 bit for bit; lane_mask: no exec branch)
+      vA = f2{mask_f(vA[0], mA), mask_f(vA[1], mA)};
+      wA = mask_f(wA, mA);
       fslot_solve_velocity_p<kSA, kP>(s, vA, wA, vB, wB);
     }
     const uint32_t x[10] = {__float_as_uint(vB[0]), __float_as_uint(vB[1]), __float_as_uint(wB),
@@ -559,6 +558,7 @@ HK_DEV void vone_family(FSlot &s, Dyn &B, int &it, bool &active, int first) {
   const bool entered = active;
   const int bA = fs_bA(s), bB = fs_bB(s), vc = fs_vcount(s);
   const bool dynA = bA < 3;
+  const uint32_t mA = lane_mask(dynA);
   v2 vA2, vB2;
   float wA, wB;
   get_vel_a(B, bA, vA2, wA);
@@ -572,13 +572,13 @@ HK_DEV void vone_family(FSlot &s, Dyn &B, int &it, bool &active, int first) {
     const bool sa = !wave_any(active && dynA);
     const bool p1 = !wave_any(active && vc != 1), p2 = !wave_any(active && vc != 2);
     if (sa) {
-      if (p1) vone_chunk<true, 1>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
-      else if (p2) vone_chunk<true, 2>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
-      else vone_chunk<true, 0>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+      if (p1) vone_chunk<true, 1>(s, dynA, mA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else if (p2) vone_chunk<true, 2>(s, dynA, mA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else vone_chunk<true, 0>(s, dynA, mA, vA, wA, vB, wB, sn, it, stop, first, active);
     } else {
-      if (p1) vone_chunk<false, 1>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
-      else if (p2) vone_chunk<false, 2>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
-      else vone_chunk<false, 0>(s, dynA, vA, wA, vB, wB, sn, it, stop, first, active);
+      if (p1) vone_chunk<false, 1>(s, dynA, mA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else if (p2) vone_chunk<false, 2>(s, dynA, mA, vA, wA, vB, wB, sn, it, stop, first, active);
+      else vone_chunk<false, 0>(s, dynA, mA, vA, wA, vB, wB, sn, it, stop, first, active);
     }
   }
   if (entered) {
@@ -604,9 +604,9 @@ struct TwoState {
 };
 // kG: some lane has retired contact 0 (it is then skipped by a per-lane branch; otherwise solved unguarded)
 template <int kP0, int kP1, bool kG>
-HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bool dA0, bool dA1, bool a1a0,
-                       bool a1b0, bool b1a0, bool b1b0, int &it, int stop, int first, bool &active, bool &on0,
-                       bool &on1) {
+HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bool dA0, bool dA1, uint32_t mA0,
+                       uint32_t mA1, bool a1a0, bool a1b0, bool b1a0, bool b1b0, int &it, int stop, int first,
+                       bool &active, bool &on0, bool &on1) {
   // the state lives in this function's own locals for the loop (selects between fields of a by-reference
   // struct turn into pointer selects, which keep the struct in scratch memory)
   f2 vA0 = t.vA0, vB0 = t.vB0, vA1 = t.vA1, vB1 = t.vB1;
@@ -619,10 +619,8 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bo
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!kG || on0) {
-        if (!dA0) {
-          vA0 = f2{0.0f, 0.0f};
-          wA0 = 0.0f;
-        }
+        vA0 = f2{mask_f(vA0[0], mA0), mask_f(vA0[1], mA0)};  // static A: +0 (lane_mask)
+        wA0 = mask_f(wA0, mA0);
         fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
         vA1 = sel2(a1a0, vA0, sel2(a1b0, vB0, vA1));
         wA1 = a1a0 ? wA0 : (a1b0 ? wB0 : wA1);
@@ -630,10 +628,8 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bo
         wB1 = b1a0 ? wA0 : (b1b0 ? wB0 : wB1);
       }
       if (on1) {
-        if (!dA1) {
-          vA1 = f2{0.0f, 0.0f};
-          wA1 = 0.0f;
-        }
+        vA1 = f2{mask_f(vA1[0], mA1), mask_f(vA1[1], mA1)};
+        wA1 = mask_f(wA1, mA1);
         fslot_solve_velocity_p<false, kP1>(s1, vA1, wA1, vB1, wB1);
         vA0 = sel2(a1a0, vA1, sel2(b1a0, vB1, vA0));
         wA0 = a1a0 ? wA1 : (b1a0 ? wB1 : wA0);
@@ -688,6 +684,7 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
   const int a0 = fs_bA(s0), b0 = fs_bB(s0);
   const int a1 = two ? fs_bA(s1) : 15, b1 = two ? fs_bB(s1) : 15;  // 15: matches no body
   const bool dA0 = a0 < 3, dA1 = a1 < 3;
+  const uint32_t mA0 = lane_mask(dA0), mA1 = lane_mask(dA1);
   const bool a1a0 = a1 == a0, a1b0 = a1 == b0, b1a0 = b1 == a0, b1b0 = b1 == b0;
   const bool sep = two && fs_isl(s0) != fs_isl(s1);
   const int vc0 = fs_vcount(s0), vc1 = two ? fs_vcount(s1) : 1;
@@ -706,24 +703,24 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
   while (wave_any(active) && wave_any(active && on0 && on1)) {
     const int stop = chunk_end(it);
     if (wave_any(active && !on0))
-      vtwo_chunk<0, 0, true>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+      vtwo_chunk<0, 0, true>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                              on1);
     else if (!wave_any(active && (vc0 != 1 || vc1 != 1)))
-      vtwo_chunk<1, 1, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+      vtwo_chunk<1, 1, false>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                               on1);
     // a wave whose running lanes agree on both point counts runs the rows without the other count's code (a
     // lane of a one-contact island rides along with contact 1 masked off, whatever kP1 says)
     else if (!wave_any(active && (vc0 != 1 || (two && vc1 != 2))))
-      vtwo_chunk<1, 2, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+      vtwo_chunk<1, 2, false>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                               on1);
     else if (!wave_any(active && (vc0 != 2 || (two && vc1 != 1))))
-      vtwo_chunk<2, 1, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+      vtwo_chunk<2, 1, false>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                               on1);
     else if (!wave_any(active && (vc0 != 2 || (two && vc1 != 2))))
-      vtwo_chunk<2, 2, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+      vtwo_chunk<2, 2, false>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                               on1);
     else
-      vtwo_chunk<0, 0, false>(s0, s1, t, two, sep, dA0, dA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
+      vtwo_chunk<0, 0, false>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                               on1);
   }
   if (entered) {

@@ -231,6 +231,25 @@ def recorded_rate_z(winner, recorded):
             "z_binomial": (float(recorded) - est) / se_b, "replicas": reps, "placements": e}
 
 
+def pin_acceptance(rows):
+    """The acceptance rule of the checkpoint pins (tests/test_gpu_checkpoints.py), as a verdict instead of asserts:
+    rates no selection touched need |z| < 3 each and sum z^2 below the chi-square 0.1 % point; rates behind a
+    best-checkpoint selection need -3 < z < Phi^-1(1 - 0.01 / n_evals).  Returns a dict with ``passed`` and the
+    statistics behind it (free chi^2 and its p-value, the violating rows)."""
+    from scipy import stats
+
+    free = [r for r in rows if not r["selected"]]
+    sel = [r for r in rows if r["selected"]]
+    chi2 = float(sum(r["z"] ** 2 for r in free))
+    crit = float(stats.chi2.ppf(0.999, len(free))) if free else float("inf")
+    bad_free = [(r["checkpoint"], r["opponent"], round(r["z"], 2)) for r in free if not abs(r["z"]) < 3]
+    bad_sel = [(r["checkpoint"], r["opponent"], round(r["z"], 2)) for r in sel
+               if not -3 < r["z"] < stats.norm.ppf(1 - 0.01 / r["n_evals"])]
+    return {"passed": not bad_free and not bad_sel and chi2 < crit, "free_chi2": chi2, "free_dof": len(free),
+            "free_chi2_crit_0.999": crit, "free_chi2_p": float(stats.chi2.sf(chi2, len(free))) if free else 1.0,
+            "violations_free": bad_free, "violations_selected": bad_sel, "n_free": len(free), "n_selected": len(sel)}
+
+
 def checkpoint_pins(fixture, replicas=64, device="cuda:0"):
     """Every shipped checkpoint against its recorded evaluation (tests/golden/checkpoint_actors.npz, written by
     tests/golden/extract_checkpoint_actors.py): each actor runs the reference's evaluation protocol on R =

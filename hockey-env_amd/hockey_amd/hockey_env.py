@@ -114,10 +114,9 @@ class HockeyEnv:
         self._step_flags = 0  # HK_STEP_* (the golden harness sets HK_STEP_SKIP_PHYSICS)
         self._host_ptrs = (self._act_np.ctypes.data_as(ctypes.c_void_p), self._inc_np.ctypes.data_as(ctypes.c_void_p),
                            self._out_np.ctypes.data_as(ctypes.c_void_p))
-        # the step's fixed call arguments: context, flags are read per call; the stream is the one current at
-        # construction (a facade is a single-stream object, like the reference env)
+        # the step's fixed call argument; the context, flags and torch's current stream are read per call, so a
+        # step is ordered on the same stream as the reset / set_state / observe calls around it
         self._step_fn = self._vec.L.hk_step_host
-        self._step_stream = self._vec._stream()
         self._ptr = {k: ctypes.c_void_p(base + off) for k, off in
                      (("obs", _OBS), ("obs2", _OBS2), ("info", _INFO), ("info2", _INFO2), ("reward", _REW),
                       ("reward2", _REW2), ("aux", _AUXI))}
@@ -195,7 +194,7 @@ class HockeyEnv:
             inc_p = None
         elif opp_inc is not True:
             self._inc_np[:] = opp_inc
-        rc = self._step_fn(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._step_stream)
+        rc = self._step_fn(self._vec._ctx, act_p, inc_p, self._step_flags, out_p, self._vec._stream())
         if rc:
             N.check(rc, "hk_step_host")
         # the snapshot: obs2 / f stay views of the step's out buffer, which only
@@ -203,7 +202,9 @@ class HockeyEnv:
         o = self._out_obs.astype(np.float64)
         self._snap = _Snap(o, self._out_obs2, self._out_f)
         f = self._out_f.tolist()  # Python floats of the record (one conversion instead of one per field)
-        obs = o if self.keep_mode else o[:16].copy()  # a fresh float64 array either way
+        # a fresh float64 array either way: the snapshot keeps o, so an in-place change of the returned obs
+        # must not reach _get_obs() (the reference returns an independent array)
+        obs = o.copy() if self.keep_mode else o[:16].copy()
         return obs, f[8], bool(f[13]), False, {"winner": int(f[0]), "reward_closeness_to_puck": f[1],
                                                "reward_touch_puck": f[2], "reward_puck_direction": f[3]}
 

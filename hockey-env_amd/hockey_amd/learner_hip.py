@@ -162,6 +162,8 @@ class FusedLearner:
         self.rng = rng
         self.L = L
         self.agent, self.ring, self.B = agent, ring, int(batch)
+        if getattr(agent, "_fused_learner", None) is not None:
+            raise RuntimeError("FusedLearner: this agent already has a fused learner (one owns its Adam state)")
         dev = agent.device
         if dev.type != "cuda":
             raise _native.HockeyNativeError("the fused learner runs on the GPU only")
@@ -217,6 +219,7 @@ class FusedLearner:
         st = self._stream()
         for group in (("actor", "target_actor"), ("q1", "q2"), ("tq1", "tq2")):
             self._pack([self.nets[k] for k in group], None, st)
+        agent._fused_learner = self  # TD3.update / TD3.load now fail loudly (TD3._no_fused)
 
     # ------------------------------------------------------------------ structs (fixed pointers)
     def _build_io(self, low, rng):

@@ -251,7 +251,20 @@ class PrioritizedRing(ReplayRing):
         return self.s[i], self.a[i], self.r[i], self.s2[i], self.d[i], iw
 
     def update_priorities(self, td):
-        self.w[self.last] = torch.clamp(td.detach(), 1e-6, 1e6)
+        """w[last] = clamp(td) with numpy's semantics for a slot drawn more than once in the batch: the LAST
+        occurrence wins (prioritized_buffer.py update_priorities).  A plain device index_put leaves the winner to
+        the scheduler, so every duplicate writes its group's last value instead (sort by (slot, position), the
+        group end by a reversed running minimum): deterministic, graph-capturable, no host sync."""
+        i = self.last
+        b = i.numel()
+        ar = torch.arange(b, device=i.device)
+        key, perm = torch.sort(i * b + ar)
+        slot = key // b
+        is_last = torch.ones(b, dtype=torch.bool, device=i.device)
+        is_last[:-1] = slot[1:] != slot[:-1]
+        end = torch.where(is_last, ar, torch.full_like(ar, b))
+        end = torch.flip(torch.cummin(torch.flip(end, [0]), 0).values, [0])
+        self.w[slot] = torch.clamp(td.detach()[perm[end]], 1e-6, 1e6)
 
 
 class TD3:
@@ -300,8 +313,17 @@ class TD3:
                 torch._foreach_mul_(tp, 1.0 - tau)
                 torch._foreach_add_(tp, sp, alpha=tau)
 
+    def _no_fused(self, what):
+        # a FusedLearner (hockey_amd.learner_hip) owns this agent's optimiser state and MFMA operand packs from the
+        # moment it is attached: an eager update would split the Adam moments, and weights loaded afterwards would
+        # not reach the packs -- fail loudly instead of training on stale state
+        if getattr(self, "_fused_learner", None) is not None:
+            raise RuntimeError(f"TD3.{what}: a fused learner is attached to this agent; update through it "
+                               "(Learner(..., fused=True)) or build a new agent")
+
     def _update_tensors(self, s, a, r, s2, d, iw=None, ring=None, train_actor=None):
         """One learner.update on a sampled batch; returns (actor loss or None, critic loss) as 0-d tensors."""
+        self._no_fused("update")
         if train_actor is None:
             self.train_step += 1
             train_actor = self.train_step % self.cfg.policy_update_freq == 0
@@ -378,6 +400,35 @@ class TD3:
             return {k: v.detach().clone() for k, v in m.state_dict().items()}
         return {"policy": sd(self.actor), "critic": sd(self.critic), "target_policy": sd(self.target_actor),
                 "target_critic": sd(self.target_critic)}
+
+    def load(self, ck):
+        """agent.load (rl/td3/agent.py:278-286): all four networks from a td3_*.pt dict (or a path, read
+        weights-only); the optimiser state is left as it is (the reference's resume starts fresh Adam moments).
+        Call before a fused Learner is attached: it packs its operands from these weights when built."""
+        self._no_fused("load")
+        if isinstance(ck, (str, bytes)) or hasattr(ck, "__fspath__"):
+            ck = load_checkpoint(ck)
+        with torch.no_grad():
+            for key, net in (("policy", self.actor), ("critic", self.critic), ("target_policy", self.target_actor),
+                             ("target_critic", self.target_critic)):
+                net.load_state_dict({k: torch.as_tensor(v) for k, v in ck[key].items()})
+
+
+def load_checkpoint(path):
+    """A td3_*.pt (``torch.load(weights_only=True)``) or the ``<net>/<param>`` npz fixture of one
+    (tests/golden/extract_resume_checkpoint.py) as the reference's {policy, critic, target_policy, target_critic}
+    dict of CPU tensors."""
+    path = str(path)
+    if path.endswith(".npz"):
+        import numpy as np
+        z = np.load(path)
+        out = {}
+        for key in z.files:
+            if "/" in key:
+                net, name = key.split("/", 1)
+                out.setdefault(net, {})[name] = torch.from_numpy(z[key])
+        return out
+    return torch.load(path, map_location="cpu", weights_only=True)
 
 
 FUSED_MIN_BATCH = 256  # fused="auto": the MFMA learner for batches of 256 and up (its chunk granularity): 0.32 ms
@@ -478,7 +529,7 @@ class Learner:
 def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_per_round=None, mode=Mode.NORMAL,
           curriculum=None, use_self_play=None, self_play_interval=None, pool_size=None, reset="seeded", log=None,
           replay_capacity=None, graphs=True, eval_fn=None, learner_batch=None, timing=False, replay_ratio=None,
-          env=None, on_step=None, episode_end="max_steps", fused="auto"):
+          env=None, on_step=None, episode_end="max_steps", fused="auto", resume_from=None):
     """Batched TD3 training (rl/training/train.py TD3Trainer.train).  Each round runs ``max_steps`` steps of
     ``n_arenas`` parallel episodes (no break on done), stores every transition, then performs the learner
     updates of those episodes at the replay ratio: ``ratio * n_arenas * max_steps / B`` updates of batch B =
@@ -503,7 +554,10 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     arena are neither stored nor counted): the semantics the reference's recorded runs were produced with --
     over the 47 000 episodes of pretrained/stage_{1,2,3}/metrics/metrics.json the return never exceeds 10.0,
     the +10 of a single goal, which the no-break loop (+10 per post-goal step) cannot produce.  A round ends
-    when every arena's episode has ended."""
+    when every arena's episode has ended.
+
+    resume_from: a td3_*.pt path, its npz fixture or a checkpoint dict: rl/main.py:66-67 ``agent.load(resume_from)``
+    before training (all four networks; fresh optimisers, noise schedule and replay)."""
     import time
     from .opponents import OpponentMix
     from .vec_env import VecHockeyEnv
@@ -515,6 +569,8 @@ def train(n_arenas=1024, rounds=10, cfg=None, device="cuda:0", seed=0, updates_p
     pool_size = cfg.self_play_pool_size if pool_size is None else pool_size
     planned = rounds * cfg.max_steps * n_arenas
     agent = TD3(cfg, device, seed, max_total_steps=planned, n_envs=n_arenas)
+    if resume_from is not None:
+        agent.load(resume_from)
     own_env = env is None
     if own_env:
         env = VecHockeyEnv(n_arenas, mode=mode, device=device, policies=("external", "external"), auto_reset=False,

@@ -140,6 +140,8 @@ class OracleWorld:
 
 
 VAR_REVERSE, VAR_NO_BLOCK, VAR_NO_SLEEP, VAR_ITERS_8_3 = 1, 2, 4, 8
+# deliberately wrong physics: negative controls of the behavioural pins (scripts/pin_power_study.py)
+VAR_REST_THRESH0, VAR_ARITH_FRIC, VAR_NO_TOI, VAR_REST_MIN = 16, 32, 64, 128
 
 
 def set_variant(flags):

@@ -51,3 +51,7 @@ def test_every_shipped_checkpoint_reproduces_its_recorded_win_rates():
     for r in sel:
         bound = stats.norm.ppf(1 - 0.01 / r["n_evals"])
         assert -3 < r["z"] < bound, (r, bound)
+    # the same rule as one verdict (hockey_amd.evaluate.pin_acceptance): the CPU power study
+    # (scripts/pin_power_study.py, tests/test_pin_power.py) applies exactly this to deliberately wrong physics
+    from hockey_amd.evaluate import pin_acceptance
+    assert pin_acceptance(rows)["passed"]

@@ -323,7 +323,7 @@ def test_step_server_survives_idle_gaps_and_interleaved_calls(monkeypatch):
             assert np.array_equal(o1[0], o0[0]) and o1[1] == o0[1] and o1[2] == o0[2] and o1[4] == o0[4], (ep, t)
             assert np.array_equal(envs["1"]._out_np, envs["0"]._out_np), (ep, t)
             if t == 20:
-                time.sleep(0.05)  # past the server's 20 ms idle limit
+                time.sleep(0.05)  # past the server's idle limit (hk_capi.cpp kSrvIdleMs)
             if t == 30:
                 for env in envs.values():
                     env._vec.get_state()  # a device call between steps
@@ -334,6 +334,62 @@ def test_step_server_survives_idle_gaps_and_interleaved_calls(monkeypatch):
     assert np.array_equal(c[0], c[1]), c
     for env in envs.values():
         env.close()
+
+
+def test_round_robin_facades_share_one_step_server():
+    """Five facades stepped round-robin (a SyncVectorEnv of Hockey-One-v0 is this) plus torch work between rounds
+    (ADVICE r04): at most one resident step server per device hands over between contexts, so no step waits for
+    another context's idle server (the failure mode: ~20 ms per step).  Every facade returns exactly what a twin
+    on the launch-per-step path returns, and the mean step time stays within 0.5 ms."""
+    import os
+    import time
+
+    from hockey_amd.hockey_env import HockeyEnv
+
+    envs = [HockeyEnv() for _ in range(5)]
+    twins = [HockeyEnv() for _ in range(5)]
+    for k, (e, t) in enumerate(zip(envs, twins)):
+        e.reset(seed=70 + k)
+        t.reset(seed=70 + k)
+    rng = np.random.default_rng(5)
+    acts = rng.uniform(-1, 1, (60, 5, 8)).astype(np.float32)
+    x = torch.ones(256, 256, device="cuda:0")
+    step_s = []
+    for t in range(60):
+        for k in range(5):
+            if t == 0:  # a context picks its step path at its first hk_step_host call
+                os.environ["HK_STEP_HOST_SERVER"] = "0"
+                try:
+                    o2, r2, d2, _, info2 = twins[k].step(acts[t, k])
+                finally:
+                    del os.environ["HK_STEP_HOST_SERVER"]
+            else:
+                o2, r2, d2, _, info2 = twins[k].step(acts[t, k])
+            t0 = time.perf_counter()
+            o, r, d, _, info = envs[k].step(acts[t, k])
+            step_s.append(time.perf_counter() - t0)
+            assert np.array_equal(o, o2) and r == r2 and d == d2 and info == info2, (t, k)
+        x = torch.tanh(x @ x) * 0.01  # torch work on the current stream between rounds
+    torch.cuda.synchronize()
+    mean_ms = 1e3 * float(np.mean(step_s[5:]))
+    print(f"round-robin facade step: mean {mean_ms:.3f} ms, p99 {1e3 * np.percentile(step_s[5:], 99):.3f} ms")
+    assert mean_ms < 0.5, mean_ms
+    for e in envs + twins:
+        e.close()
+
+
+def test_keep_mode_step_returns_an_independent_obs():
+    """the float64 obs step() returns is the caller's; changing it in place leaves env._get_obs()
+    alone (the reference builds a fresh array per call)."""
+    from hockey_amd.hockey_env import HockeyEnv
+
+    env = HockeyEnv()
+    env.reset(seed=3)
+    o, *_ = env.step(np.zeros(8, np.float32))
+    keep = env._get_obs().copy()
+    o *= 0.0
+    assert np.array_equal(env._get_obs(), keep) and not np.array_equal(o, keep)
+    env.close()
 
 
 # ------------------------------------------------------------------------------------------------ behaviour

@@ -107,25 +107,39 @@ def test_fused_learner_matches_reference_learner_g9b():
     assert not bad, bad[:8]
 
 
-def test_fused_learner_matches_eager_learner_on_ring():
+@pytest.mark.parametrize("batch,updates,per,wd", [(4096, 8, False, 0.0), (16384, 6, False, 0.0),
+                                                   (4096, 6, True, 0.0), (4096, 6, False, 1e-3)],
+                         ids=["b4096", "b16384_c5", "per", "weight_decay"])
+def test_fused_learner_matches_eager_learner_on_ring(batch, updates, per, wd):
     """Fused vs eager (PyTorch) learner from the same weights and ring, with the same torch RNG stream (slots, then
-    target noise; the fused learner's torch-RNG mode): 8 updates of 4096 samples."""
-    cfg = TD3Config()
+    target noise; the fused learner's torch-RNG mode): critic and actor updates at 4096 samples, at C5's production
+    batch of 16 384 (bench c5_round, train(learner_batch=16384)), with prioritized replay (importance weights, the
+    weighted smooth-L1, TD-error priorities written back: rl/replay/prioritized_buffer.py, learner.py:163-210; each
+    learner on its own copy of the ring, whose weights must agree too) and with Adam's L2 weight decay
+    (rl/td3/agent.py:160-167 wd_q / wd_pol)."""
+    from hockey_amd.td3 import PrioritizedRing
+
+    cfg = TD3Config(prioritized_replay=per, wd_q=wd, wd_pol=wd)
     torch.manual_seed(7)
     cap = 50_000
-    ring_e = ReplayRing(cap, device=DEV)
     s, s2 = torch.randn(cap, 18, device=DEV), torch.randn(cap, 18, device=DEV)
     a = torch.rand(cap, 4, device=DEV) * 2 - 1
     r, d = torch.randn(cap, device=DEV), (torch.rand(cap, device=DEV) < 0.1).float()
-    ring_e.push(s, a, r, s2, d)
+    rings = []
+    for _ in range(2 if per else 1):
+        ring = PrioritizedRing(cap, device=DEV, beta=cfg.beta) if per else ReplayRing(cap, device=DEV)
+        ring.push(s, a, r, s2, d)
+        rings.append(ring)
+    ring_e, ring_f = rings[0], rings[-1]
     eager, fused = TD3(cfg, device=DEV, seed=3), TD3(cfg, device=DEV, seed=3)
-    le = Learner(eager, ring_e, 4096, graphs=False, fused=False)
-    lf = Learner(fused, ring_e, 4096, graphs=False, fused=True, fused_rng="torch")
-    for k in range(8):
+    le = Learner(eager, ring_e, batch, graphs=False, fused=False)
+    lf = Learner(fused, ring_f, batch, graphs=False, fused=True, fused_rng="torch")
+    for k in range(updates):
         torch.manual_seed(100 + k)
         le._one()
         torch.manual_seed(100 + k)
         lf._one()
+    assert eager.train_step == fused.train_step == updates
     ce, ae = le.take_losses()
     cf, af = lf.take_losses()
     assert abs(ce - cf) <= LOSS_RTOL * max(1.0, abs(ce)) and abs(ae - af) <= LOSS_RTOL * max(1.0, abs(ae)), (ce, cf, ae, af)
@@ -135,6 +149,9 @@ def test_fused_learner_matches_eager_learner_on_ring():
         for (kk, ve), (_, vf) in zip(ne.state_dict().items(), nf.state_dict().items()):
             worst = max(worst, float((ve - vf).abs().max()))
     assert worst <= PARAM_ATOL, worst
+    if per:  # the priorities written back agree (same slots, TD errors within fp32 summation order)
+        wdiff = (ring_e.w[:cap] - ring_f.w[:cap]).abs() / ring_e.w[:cap].abs().clamp_min(1.0)
+        assert float(wdiff.max()) <= 1e-4, float(wdiff.max())
 
 
 def test_fused_graph_replay_equals_fused_eager():
@@ -345,3 +362,24 @@ def test_operand_pack_layout_matches_numpy_restatement():
         assert ref.size == PACK_FLOATS
         got = nb.pack.cpu().numpy()
         assert np.array_equal(got, ref), (key, int(np.argmax(got != ref)))
+
+
+def test_eager_update_and_load_fail_loudly_with_a_fused_learner_attached():
+    """a FusedLearner owns its agent's Adam moments and MFMA operand packs, so an eager agent.update()
+    (split optimiser state) or agent.load() (weights the packs would not see) afterwards raises instead of training
+    on stale state; a second FusedLearner on the same agent is refused too."""
+    from hockey_amd.learner_hip import FusedLearner
+
+    agent = TD3(TD3Config(), device=DEV, seed=4)
+    ring = ReplayRing(4096, device=DEV)
+    ring.push(torch.zeros(4096, 18, device=DEV), torch.zeros(4096, 4, device=DEV), torch.zeros(4096, device=DEV),
+              torch.zeros(4096, 18, device=DEV), torch.zeros(4096, device=DEV))
+    ck = agent.checkpoint()
+    FusedLearner(agent, ring, 256)
+    s = torch.zeros(8, 18, device=DEV)
+    with pytest.raises(RuntimeError, match="fused learner"):
+        agent.update(s, torch.zeros(8, 4, device=DEV), torch.zeros(8, device=DEV), s, torch.zeros(8, device=DEV))
+    with pytest.raises(RuntimeError, match="fused learner"):
+        agent.load(ck)
+    with pytest.raises(RuntimeError, match="fused learner"):
+        FusedLearner(agent, ring, 256)

@@ -395,6 +395,33 @@ def test_episode_end_done_stores_only_running_episodes():
     assert stored < n * len(seen) or len(seen) == 251
 
 
+def test_resume_from_loads_all_four_networks():
+    """train(resume_from=...) = rl/main.py:66-67 agent.load: policy, critic and both targets come from the checkpoint
+    (tests/golden/stage1_best_full.npz, the reference's stage-1 best = the Stage II resume point); with no update the
+    trained agent's checkpoint() is the fixture bit for bit, and the resumed actor acts from the first step."""
+    from hostcheck import HostTorchEnv
+
+    from hockey_amd.td3 import load_checkpoint, train
+
+    ck = load_checkpoint(os.path.join(GOLDEN, "stage1_best_full.npz"))
+    assert set(ck) == {"policy", "critic", "target_policy", "target_critic"}
+    n = 4
+    env = HostTorchEnv(n, policies=("external", "external"))
+    cfg = TD3Config(max_steps=5, start_steps=0, batch_size=32, use_self_play=False, curriculum_name="stage2",
+                    use_noise_annealing=False, action_noise_scale=1e-30)
+    acts = []
+    agent, st = train(n_arenas=n, rounds=1, cfg=cfg, device="cpu", seed=7, env=env, graphs=False,
+                      updates_per_round=0, resume_from=ck, on_step=lambda o, a, r, o2, d, res: acts.append((o, a)))
+    got = agent.checkpoint()
+    for net in ck:
+        assert set(got[net]) == set(ck[net]), net
+        for k, v in ck[net].items():
+            assert torch.equal(got[net][k], v), (net, k)
+    o, a = acts[0]
+    with torch.no_grad():
+        assert torch.allclose(a, agent.actor(o), atol=1e-6)
+
+
 def test_learner_matches_reference_learner_g9b_wide():
     """G9b (hidden 256, batch 256: the C5 network shapes; tests/golden/make_td3_golden.py --wide): the eager learner on
     the CPU reproduces the reference's TD3Learner losses and parameters (float32 rounding only)."""
