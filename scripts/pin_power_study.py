@@ -109,13 +109,60 @@ def pins(meta, actors, replicas, vel_ref=False):
     return rows
 
 
+def detectable_shift(rows):
+    """The smallest uniform shift delta (win-rate points, simulator minus recorded) of every free rate that takes the
+    free chi^2 of ``rows`` to the acceptance rule's 0.1 % critical value: the resolution of the pin as a whole."""
+    from scipy import stats
+
+    free = [r for r in rows if not r["selected"]]
+    crit = stats.chi2.ppf(0.999, len(free))
+    out = {}
+    for sign in (1, -1):
+        lo, hi = 0.0, 1.0
+        for _ in range(60):
+            mid = 0.5 * (lo + hi)
+            chi2 = sum(((r["recorded"] - (r["estimate"] + sign * mid)) / r["se"]) ** 2 for r in free)
+            lo, hi = (lo, mid) if chi2 >= crit else (mid, hi)
+        out["up" if sign > 0 else "down"] = round(100 * hi, 2)
+    return out
+
+
+def summarize(out):
+    """Per variant: pass / fail, free chi^2, the stage-1 best strong z, and the paired shift of the 20 simulated
+    rates against base (common random numbers: same placements, phases and Philox streams), in win-rate points."""
+    base = out["variants"].get("base")
+    table = {}
+    for name, v in out["variants"].items():
+        t = {"wrong_physics": v["wrong_physics"], "passed": v["acceptance"]["passed"],
+             "free_chi2": round(v["acceptance"]["free_chi2"], 2), "stage1_best_strong_z": round(v["stage1_best_strong_z"], 2),
+             "max_abs_z": round(max(abs(r["z"]) for r in v["rows"]), 2)}
+        if base:
+            d = np.array([100 * (r["estimate"] - b["estimate"]) for r, b in zip(v["rows"], base["rows"])])
+            t.update(shift_mean_pts=round(float(d.mean()), 2), shift_rms_pts=round(float(np.sqrt((d ** 2).mean())), 2),
+                     shift_max_abs_pts=round(float(np.abs(d).max()), 2))
+        table[name] = t
+    if base:
+        table["_pin_resolution_pts"] = detectable_shift(base["rows"])
+    return table
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--replicas", type=int, default=64)
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--summarize", action="store_true", help="only recompute the summary of an existing --out")
     args = ap.parse_args()
+    if args.summarize:
+        with open(args.out) as f:
+            out = json.load(f)
+        out["summary"] = summarize(out)
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
+        for name, t in out["summary"].items():
+            print(name, t)
+        return
     if args.threads:
         torch.set_num_threads(args.threads)
     meta, actors = load_actors()
@@ -145,8 +192,14 @@ def main():
         if args.out:
             with open(args.out, "w") as f:
                 json.dump(out, f, indent=1)
-    if not args.out:
+    out["summary"] = summarize(out)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
+    else:
         print(json.dumps(out, indent=1))
+    for name, t in out["summary"].items():
+        print(name, t, file=sys.stderr)
 
 
 if __name__ == "__main__":
