@@ -22,6 +22,15 @@ import numpy as np
 import torch
 
 from . import _native as N
+
+_getraw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(index):
+    """torch's current stream on device ``index`` as an integer hipStream_t."""
+    if _getraw is not None:
+        return _getraw(index)
+    return torch.cuda.current_stream(index).cuda_stream
 from .constants import Mode, parse_mode
 from .placement import np_random, placement
 
@@ -52,6 +61,7 @@ class VecHockeyEnv:
             raise N.HockeyNativeError("VecHockeyEnv needs a ROCm GPU (gfx950); the hot path has no CPU fallback")
         self.L = N.lib()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.n = int(n_arenas)
         self.keep_mode = bool(keep_mode)
         self.mode = parse_mode(mode)
@@ -90,7 +100,9 @@ class VecHockeyEnv:
         self.record_buf = torch.zeros((n, N.RECORD_DIM), dtype=torch.float64, device=d)
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # torch's current stream on this device as a raw hipStream_t: the C accessor, without building a
+        # torch.cuda.Stream object (the single-env facade reads it on every step)
+        return ctypes.c_void_p(_raw_stream(self._dev_index))
 
     def close(self):
         if getattr(self, "_ctx", None):
