@@ -97,3 +97,28 @@ if ev.any():
     print(f"lanes with >= 1 TOI event: {ev.mean() * 100:.2f}% of lane-steps; their own phase cycles (mean):")
     for k in (5, 6, 7, 8, 9, 10, 11):
         print(f"  {PH[k]:22s} {E[:, k].mean():10.0f}")
+# what bounds the launch (r05): the per-step maximum over waves, recomputed with each class of wave removed -- the most
+# a faster loop for that class could save (its waves would still cost something).  Classes: the contact count of the
+# wave's 180-iteration island lanes (0: none), a lane with >= 30 position passes, a lane with a 180-iteration TOI solve.
+wave_cyc = wave  # [steps, waves]
+ncl_sw = ncl.reshape(steps, n // 64)
+pit_sw = W[:, :, 4].max(1).reshape(steps, n // 64)
+vtoi_sw = W[:, :, 3].max(1).reshape(steps, n // 64)
+base = wave_cyc.max(1).mean()
+print(f"launch bound (mean over steps of the slowest wave): {base:.0f} cycles")
+classes = {f"180-iteration island with {c} contacts": ncl_sw == c for c in (1, 2, 3, 4)}
+classes["any 180-iteration island lane"] = ncl_sw >= 1
+classes["position loop >= 30 passes"] = pit_sw >= 30
+classes["TOI solve >= 100 iterations"] = vtoi_sw >= 100
+for nm, m in classes.items():
+    rest = np.where(m, 0, wave_cyc).max(1).mean()
+    share = m[np.arange(steps), wave_cyc.argmax(1)].mean()
+    print(f"  {nm:40s} waves/step {m.sum(1).mean():7.1f}  owns the slowest wave in {share * 100:5.1f}% of steps  "
+          f"max without them {rest:9.0f} ({(1 - rest / base) * 100:4.1f}% lower)")
+sw = wave_cyc.argmax(1)
+print("slowest wave of each step: phase cycles by its 180-iteration contact class")
+for c in (0, 1, 2, 3, 4):
+    m = ncl_sw[np.arange(steps), sw] == c
+    if m.any():
+        print(f"  class {c}: {m.sum():3d} steps  total {wave_cyc[np.arange(steps), sw][m].mean():9.0f}  " +
+              " ".join(f"{PH[k].split('+')[0]} {slow[m, k].mean():7.0f}" for k in (1, 3, 4, 5, 7, 11)))
