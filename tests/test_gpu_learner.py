@@ -383,3 +383,45 @@ def test_eager_update_and_load_fail_loudly_with_a_fused_learner_attached():
         agent.load(ck)
     with pytest.raises(RuntimeError, match="fused learner"):
         FusedLearner(agent, ring, 256)
+
+
+def test_resume_from_stage1_best_on_the_gpu_with_the_fused_learner():
+    """The Stage II resume (scripts/noise_study.py --protocol stage2): train(resume_from=stage1_best_full.npz) on GPU
+    arenas with the fused learner attached.  Before any update the agent's four networks are the reference's stage-1
+    best bit for bit and the fused learner's operand packs are those of these weights (its first critic / actor updates
+    from the resumed weights equal the eager learner's from the same weights: fused == eager after 4 updates), and
+    the resumed actor plays the weak bot like the stage-1 best checkpoint (recorded 0.99, simulated 0.967: >= 0.9 over
+    200 games)."""
+    from hockey_amd.evaluate import evaluate
+    from hockey_amd.td3 import load_checkpoint, train
+
+    ck = load_checkpoint(os.path.join(GOLDEN, "stage1_best_full.npz"))
+    cfg = TD3Config(max_steps=20, curriculum_name="stage2", use_self_play=False, start_steps=0)
+    agent, st = train(n_arenas=256, rounds=1, cfg=cfg, device=DEV, seed=11, updates_per_round=0, fused=True,
+                      resume_from=ck, learner_batch=256)
+    got = agent.checkpoint()
+    for net in ck:
+        for k, v in ck[net].items():
+            assert torch.equal(got[net][k].cpu(), v), (net, k)
+    agent.actor.eval()
+    w = evaluate(agent.actor, episodes=200, seed=420, weak_opponent=True, device=DEV)
+    assert w["win"] >= 0.9, w
+    # fused from the resumed weights == eager from the same weights
+    torch.manual_seed(3)
+    cap = 20_000
+    ring = ReplayRing(cap, device=DEV)
+    ring.push(torch.randn(cap, 18, device=DEV), torch.rand(cap, 4, device=DEV) * 2 - 1, torch.randn(cap, device=DEV),
+              torch.randn(cap, 18, device=DEV), (torch.rand(cap, device=DEV) < 0.1).float())
+    eager, fused = TD3(TD3Config(), device=DEV, seed=1), TD3(TD3Config(), device=DEV, seed=1)
+    eager.load(ck)
+    fused.load(ck)
+    le = Learner(eager, ring, 1024, graphs=False, fused=False)
+    lf = Learner(fused, ring, 1024, graphs=False, fused=True, fused_rng="torch")
+    for k in range(4):
+        torch.manual_seed(50 + k)
+        le._one()
+        torch.manual_seed(50 + k)
+        lf._one()
+    worst = max(float((a - b).abs().max()) for ne, nf in ((eager.actor, fused.actor), (eager.critic, fused.critic))
+                for a, b in zip(ne.state_dict().values(), nf.state_dict().values()))
+    assert worst <= PARAM_ATOL, worst
