@@ -113,6 +113,10 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--episodes", type=int, default=10_000)
     ap.add_argument("--curriculum", default="noise_study")
+    ap.add_argument("--protocol", choices=["scratch", "stage2"], default="scratch",
+                    help="stage2: the report's Stage II setup (definitions.py:93-114): resume from the stage-1 best "
+                         "checkpoint, curriculum stage2, lr 3e-4, noise floor 0.06 (as scripts/noise_study.py)")
+    ap.add_argument("--final-games", type=int, default=1000)
     ap.add_argument("--episode-end", choices=["done", "max_steps"], default="done")
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--out", required=True)
@@ -123,15 +127,25 @@ def main():
 
     set_global_seed(args.seed)  # rl/main.py:86
     cfg = TD3Config()
-    for k, v in dict(curriculum_name=args.curriculum, noise_mode=NOISES[args.noise], prioritized_replay=False,
-                     use_self_play=False, use_noise_annealing=True).items():  # definitions.py:10-31 noise_study
+    over = dict(curriculum_name=args.curriculum, noise_mode=NOISES[args.noise], prioritized_replay=False,
+                use_self_play=False, use_noise_annealing=True)  # definitions.py:10-31 noise_study
+    if args.protocol == "stage2":
+        over.update(curriculum_name="stage2", lr_q=3e-4, lr_pol=3e-4, noise_min_scale=0.06)
+    for k, v in over.items():
         setattr(cfg, k, v)
     train_env = OracleHockeyEnv()
     evaluators = {"strong": Evaluator(OracleHockeyOne(H, False), episodes=cfg.eval_episodes),
                   "weak": Evaluator(OracleHockeyOne(H, True), episodes=cfg.eval_episodes)}
     agent = TD3Agent(env=train_env, config=cfg, h=256, max_total_steps=args.episodes * cfg.max_steps, seed=args.seed)
-    out = {"study": "reference rl/ loop on the oracle", "noise": args.noise, "seed": args.seed, "episodes": args.episodes,
-           "curriculum": args.curriculum, "episode_end": args.episode_end, "evals": [], "best": None}
+    if args.protocol == "stage2":  # agent.load (rl/td3/agent.py:278-286), read weights-only
+        ck = torch.load(os.path.join(REF, "pretrained", "stage_1", "models", "td3_best.pt"), map_location="cpu",
+                        weights_only=True)
+        for key, net in (("policy", agent.policy), ("critic", agent.critic), ("target_policy", agent.target_policy),
+                         ("target_critic", agent.target_critic)):
+            net.load_state_dict(ck[key])
+    out = {"study": "reference rl/ loop on the oracle", "protocol": args.protocol, "noise": args.noise,
+           "seed": args.seed, "episodes": args.episodes, "curriculum": cfg.curriculum_name,
+           "episode_end": args.episode_end, "evals": [], "best": None}
     t0 = time.time()
     best = {"score": float("-inf")}
 
@@ -170,6 +184,7 @@ def main():
                    "wall_s": round(time.time() - t0, 1)}
             if score > best["score"] + 0.01:  # rl/utils/model_manager.py:15-23
                 best["score"] = score
+                best["state"] = {k: v.detach().clone() for k, v in self.agent.policy.state_dict().items()}
                 out["best"] = dict(rec)
             out["evals"].append(rec)
             with open(args.out, "w") as f:
@@ -183,6 +198,16 @@ def main():
                  metrics_dir=os.path.join("/tmp", "reflooprun"), plot_dir=os.path.join("/tmp", "reflooprun"),
                  max_episodes=args.episodes)
     tr.train()
+    if "state" in best:  # the best checkpoint re-evaluated on fresh placements (as scripts/noise_study.py)
+        agent.policy.load_state_dict(best["state"])
+        seed0 = agent.seed
+        agent.seed = 100_000
+        fin = {"games": args.final_games}
+        for opp in ("strong", "weak"):
+            wr, rr = Evaluator(OracleHockeyOne(H, opp == "weak"), episodes=args.final_games).evaluate(agent)
+            fin[f"wr_{opp}"], fin[f"r_{opp}"] = wr, rr
+        agent.seed = seed0
+        out["final_eval"] = fin
     out["wall_s"] = round(time.time() - t0, 1)
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
