@@ -7,7 +7,7 @@
 #   tests    the GPU suite only ([pytest -k expression])
 #   bench    bench.py with the given arguments, then rocprofv3 --kernel-trace --stats of the same command
 #   noise    scripts/noise_study.py: <protocol> <seed | noise:seed>... -> every noise x seed (or the named pairs)
-#            side by side, one process each
+#            side by side, one process each; protocol sp_per takes p<0|1>s<0|1>:seed (PER, self-play switches)
 #   learner  scripts/learner_profile.py + rocprofv3 kernel stats of it
 # Every GPU step runs under its own time limit; the script stops at the first failure (no retries).
 set -u
@@ -62,8 +62,12 @@ case "$JOB" in
     done
     for r in $runs; do
       noise=${r%%:*}; seed=${r##*:}
+      extra=""
+      case "$noise" in  # sp_per: the token names the switches, p<0|1>s<0|1> (prioritized replay, self-play)
+        p?s?) extra="--per ${noise:1:1} --sp ${noise:3:1}"; noise=ou ;;
+      esac
       OMP_NUM_THREADS=1 timeout -k 10 ${T_RUN:-1080} python -u scripts/noise_study.py --protocol "$PROTO" \
-        --noise $noise --seed $seed --out "$O" > "$O/${PROTO}_${noise}_s$seed.log" 2>&1 &
+        --noise $noise --seed $seed $extra --out "$O" > "$O/${PROTO}_${r/:/_s}.log" 2>&1 &
       pids="$pids $!"
     done
     rc=0

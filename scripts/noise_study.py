@@ -52,16 +52,35 @@ REFERENCE = {"gaussian": {"wr_weak": (92.50, 4.48), "wr_strong": (81.00, 0.47), 
                          "r_strong": (5.51, 1.51)}}
 
 
-def config(protocol, noise):
+# template.tex:313-345 (Table "Final evaluation results", mean +- std over three seeds, percent / return)
+REFERENCE_SP_PER = {(False, False): {"wr_weak": (93.07, 3.75), "wr_strong": (78.27, 3.07), "r_weak": (8.33, 0.66),
+                                     "r_strong": (5.00, 0.70)},
+                    (False, True): {"wr_weak": (90.73, 5.90), "wr_strong": (72.60, 7.63), "r_weak": (7.62, 1.26),
+                                    "r_strong": (4.06, 1.56)},
+                    (True, False): {"wr_weak": (75.80, 9.18), "wr_strong": (66.07, 4.69), "r_weak": (4.22, 2.00),
+                                    "r_strong": (1.99, 1.04)},
+                    (True, True): {"wr_weak": (78.27, 2.23), "wr_strong": (65.33, 5.14), "r_weak": (4.71, 0.54),
+                                   "r_strong": (1.78, 1.01)}}
+
+
+def config(protocol, noise, per=False, sp=False):
     common = dict(noise_mode=NOISES[noise], prioritized_replay=False, use_self_play=False, use_noise_annealing=True)
     if protocol == "scratch":
         return TD3Config(curriculum_name="noise_study", **common), None
+    if protocol == "sp_per":
+        # definitions.py:34-66 prioritized_selfplay_study: resume from weak_10k/td3_best.pt (= pretrained/stage_1 best,
+        # pretrained/stage_2/config/run_info.json), curriculum "ablation" (= STAGE_2), OU noise, annealing, PER and
+        # self-play switched, every other field at config.py's defaults (lr 4e-4, self-play interval 250, pool 12)
+        return TD3Config(curriculum_name="ablation", noise_mode="ornstein-uhlenbeck", use_noise_annealing=True,
+                         prioritized_replay=per, use_self_play=sp), RESUME
     return TD3Config(curriculum_name="stage2", lr_q=3e-4, lr_pol=3e-4, noise_min_scale=0.06, **common), RESUME
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--protocol", choices=["scratch", "stage2"], required=True)
+    ap.add_argument("--protocol", choices=["scratch", "stage2", "sp_per"], required=True)
+    ap.add_argument("--per", type=int, default=0, help="sp_per: prioritized replay on (1) / off (0)")
+    ap.add_argument("--sp", type=int, default=0, help="sp_per: self-play on (1) / off (0)")
     ap.add_argument("--noise", choices=sorted(NOISES), required=True)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--arenas", type=int, default=20)
@@ -71,16 +90,18 @@ def main():
     ap.add_argument("--learner", choices=["auto", "fused", "eager"], default="auto")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "noise_study"))
     args = ap.parse_args()
-    cfg, resume = config(args.protocol, args.noise)
+    cfg, resume = config(args.protocol, args.noise, bool(args.per), bool(args.sp))
     n = args.arenas
     rounds = args.episodes // n
     dev = "cuda:0"
     os.makedirs(args.out, exist_ok=True)
-    stem = os.path.join(args.out, f"{args.protocol}_{args.noise}_s{args.seed}")
-    out = {"protocol": args.protocol, "noise": args.noise, "seed": args.seed, "config": vars(cfg),
+    name = f"{args.protocol}_{args.noise}" if args.protocol != "sp_per" else f"sp_per_p{args.per}_sp{args.sp}"
+    stem = os.path.join(args.out, f"{name}_s{args.seed}")
+    ref = REFERENCE[args.noise] if args.protocol != "sp_per" else REFERENCE_SP_PER[(bool(args.per), bool(args.sp))]
+    out = {"protocol": args.protocol, "noise": args.noise if args.protocol != "sp_per" else "ou", "seed": args.seed,
+           "per": bool(cfg.prioritized_replay), "self_play": bool(cfg.use_self_play), "config": vars(cfg),
            "resume_from": None if resume is None else os.path.relpath(resume, ROOT), "arenas": n,
-           "episodes": rounds * n, "eval_episodes": args.eval_episodes, "reference": REFERENCE[args.noise],
-           "evals": [], "best": None}
+           "episodes": rounds * n, "eval_episodes": args.eval_episodes, "reference": ref, "evals": [], "best": None}
     t0 = time.time()
     best = {"score": float("-inf")}
 

@@ -15,9 +15,6 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from noise_study import REFERENCE  # noqa: E402
-
 KEYS = (("wr_weak", 100.0), ("wr_strong", 100.0), ("r_weak", 1.0), ("r_strong", 1.0))
 
 
@@ -28,7 +25,8 @@ def load(dirs):
             r = json.load(open(f))
             if "final_eval" not in r:
                 continue
-            runs[(r["protocol"], r["noise"], r["seed"])] = r  # later directories override earlier partial runs
+            label = r["noise"] if r["protocol"] != "sp_per" else f"per{int(r['per'])}_sp{int(r['self_play'])}"
+            runs[(r["protocol"], label, r["seed"])] = r  # later directories override earlier partial runs
     return runs
 
 
@@ -38,7 +36,8 @@ def main():
            "protocols": {}}
     for proto in sorted({k[0] for k in runs}):
         pr = {}
-        for noise in ("gaussian", "ou", "pink", "uniform"):
+        labels = sorted({k[1] for k in runs if k[0] == proto})
+        for noise in labels:
             rs = [runs[k] for k in sorted(runs) if k[0] == proto and k[1] == noise]
             if not rs:
                 continue
@@ -46,7 +45,7 @@ def main():
             for key, scale in KEYS:
                 v = np.array([r["final_eval"][key] * scale for r in rs])
                 m, sd1 = float(v.mean()), float(v.std(ddof=1)) if len(v) > 1 else 0.0
-                rm, rsd = REFERENCE[noise][key]
+                rm, rsd = rs[0]["reference"][key]
                 se = math.sqrt(sd1 ** 2 / len(v) + rsd ** 2 / 3)
                 row[key] = {"values": [round(float(x), 3) for x in v], "mean": round(m, 3), "std": round(sd1, 3),
                             "std_ddof0": round(float(v.std()), 3), "reference": [rm, rsd],
