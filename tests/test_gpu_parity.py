@@ -493,3 +493,39 @@ def test_partial_wave_lockstep_vs_oracle(oracle, n):
     assert "field" not in out, out
     out = _bench_path_lockstep(oracle, n, 200, 2, ("external", "weak"), seed=80 + n, external=True)
     assert "field" not in out, out
+
+
+def test_rejected_calls_leave_the_context_intact():
+    """Every argument check on a live context fails with HK_E_INVALID before it launches anything (a missing
+    io.actions for an external player, n_steps < 1, hk_step_host on a multi-arena context, a bad player / policy id,
+    a missing counters buffer), and the context then steps on exactly as a twin that never saw the bad calls:
+    bit-identical obs, reward, done and state after 40 steps."""
+    import ctypes
+
+    n = 100
+    env, twin = (_vec(n, policies=("external", "strong"), auto_reset=True, seed=11) for _ in range(2))
+    L = env.L
+    io = N.StepIO()
+    io.obs = env.obs_buf.data_ptr()
+    assert L.hk_step(env._ctx, ctypes.byref(io), env._stream()) == -1 and b"io->actions is NULL" in L.hk_last_error()
+    acts = torch.rand((n, 8), device="cuda:0") * 2 - 1
+    io.actions = acts.data_ptr()
+    for k in (0, -3):
+        assert L.hk_rollout(env._ctx, k, ctypes.byref(io), env._stream()) == -1 and b"n_steps" in L.hk_last_error()
+    host = (ctypes.c_float * 64)()
+    hp = ctypes.cast(host, ctypes.c_void_p)
+    assert L.hk_step_host(env._ctx, hp, hp, 0, hp, None) == -1 and b"single-arena" in L.hk_last_error()
+    for player, pol in ((2, 0), (-1, 0), (1, 99)):
+        assert L.hk_set_policy(env._ctx, player, pol) == -1 and b"hk_set_policy" in L.hk_last_error()
+    assert L.hk_counters(env._ctx, None, env._stream()) == -1
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    for _ in range(40):
+        a = torch.rand((n, 8), device="cuda:0", generator=g) * 2 - 1
+        r1, r2 = env.step(a), twin.step(a)
+        for f in ("obs", "reward", "done", "info"):
+            assert torch.equal(getattr(r1, f), getattr(r2, f)), f
+    s1, s2 = env.get_state(), twin.get_state()
+    for x, y in zip(s1, s2):
+        assert torch.equal(x, y)
+    env.close()
+    twin.close()

@@ -202,3 +202,71 @@ def test_learner_adam_rejects_incomplete_io_before_any_launch():
     assert L.hkl_adam(ctypes.byref(io), None) == 1
     io.n_seg = 0
     assert L.hkl_adam(ctypes.byref(io), None) == 1
+
+
+def test_abi_rejects_invalid_arguments_before_any_launch():
+    """Every entry point checks its arguments on the host and fails with HK_E_INVALID and a message naming itself
+    (include/hockey.h: 0 or a negative HK_E* code, hk_last_error() describes it) -- the status-code contract the
+    reference's Python callers get as exceptions.  No GPU needed: nothing here reaches a HIP call, except a
+    well-formed hk_create, which on a host without a gfx950 device must fail with HK_E_DEVICE and leave *out NULL."""
+    from hockey_amd import _native as N
+
+    L = N.lib()
+    E_INVALID, E_DEVICE = -1, -4
+
+    def cfg(**kw):
+        c = N.Config()
+        c.keep_mode, c.mode, c.auto_reset, c.vel_ref_semantics, c.seed, c.arena_offset, c.diag_flags = 1, 0, 0, 0, 0, 0, 0
+        c.policy[0] = c.policy[1] = 0
+        for k, v in kw.items():
+            if k == "policy":
+                c.policy[0], c.policy[1] = v
+            else:
+                setattr(c, k, v)
+        return c
+
+    def err():
+        return L.hk_last_error().decode()
+
+    out = ctypes.c_void_p(1234)
+    assert L.hk_create(0, 64, ctypes.byref(cfg()), None) == E_INVALID and "out is NULL" in err()
+    for n in (0, -5, (1 << 30) + 1):
+        assert L.hk_create(0, n, ctypes.byref(cfg()), ctypes.byref(out)) == E_INVALID, n
+        assert "bad n_arenas" in err() and out.value is None
+    assert L.hk_create(0, 64, None, ctypes.byref(out)) == E_INVALID and "cfg is NULL" in err()
+    for bad, msg in ((dict(mode=3), "bad mode"), (dict(mode=-1), "bad mode"), (dict(policy=(9, 0)), "bad policy"),
+                     (dict(policy=(0, -2)), "bad policy"), (dict(diag_flags=1 << 7), "unknown diag_flags")):
+        assert L.hk_create(0, 64, ctypes.byref(cfg(**bad)), ctypes.byref(out)) == E_INVALID, bad
+        assert msg in err(), (bad, err())
+
+    io = N.StepIO()
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    cnt = (ctypes.c_int64 * 16)()
+    i64 = ctypes.c_int64()
+    calls = {"hk_set_policy": lambda: L.hk_set_policy(None, 0, 0),
+             "hk_reset": lambda: L.hk_reset(None, None, None, None, None, None),
+             "hk_step": lambda: L.hk_step(None, ctypes.byref(io), None),
+             "hk_rollout": lambda: L.hk_rollout(None, 4, ctypes.byref(io), None),
+             "hk_step_host": lambda: L.hk_step_host(None, p, p, 0, p, None),
+             "hk_get_state": lambda: L.hk_get_state(None, p, p, None),
+             "hk_set_state": lambda: L.hk_set_state(None, p, p, None, None),
+             "hk_observe": lambda: L.hk_observe(None, p, p, None),
+             "hk_info": lambda: L.hk_info(None, p, p, p, p, None),
+             "hk_opponent_phase": lambda: L.hk_opponent_phase(None, p, p, None),
+             "hk_opponent_phase3": lambda: L.hk_opponent_phase3(None, p, p, None),
+             "hk_counters": lambda: L.hk_counters(None, cnt, None),
+             "hk_reset_counters": lambda: L.hk_reset_counters(None, None),
+             "hk_bytes_per_step": lambda: L.hk_bytes_per_step(None, ctypes.byref(i64), ctypes.byref(i64))}
+    for name, call in calls.items():
+        assert call() == E_INVALID, name
+        assert err().startswith(name + ":") and "NULL" in err(), (name, err())
+    assert L.hk_num_arenas(None) == 0
+    L.hk_destroy(None)  # a no-op, as free(NULL)
+
+    rc = L.hk_create(0, 64, ctypes.byref(cfg()), ctypes.byref(out))
+    if rc == 0:  # a gfx950 device is present: the well-formed call succeeds
+        L.hk_destroy(out)
+    else:
+        assert rc == E_DEVICE and out.value is None, (rc, err())
+        assert "device" in err()
