@@ -686,12 +686,31 @@ __global__ void __launch_bounds__(256) adam_kernel(hkl_adam_io io) {
     const int64_t k = e - base;
     const int64_t rr = k / S.cols, cc = k % S.cols;
     const float *src = S.src + rr * S.ld + cc;
-    // 16 partial sums: 16 slab loads in flight per thread (the reduction is bound by memory-level parallelism:
-    // ~2 workgroups per CU at the C5 parameter counts), summed in a fixed tree
+    // 16 partial sums (chunk c into p16[c & 15], in increasing c), summed in a fixed tree; up to 64 slab loads in
+    // flight per thread (the reduction is bound by memory-level parallelism: ~2 workgroups per CU at the C5
+    // parameter counts)
     float p16[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) p16[u] = 0.0f;
     int c = 0;
+    for (; c + 64 <= S.chunks; c += 64) {  // four rounds' loads in flight at once, added in the same order
+      float q[64];
+#pragma unroll
+      for (int u = 0; u < 64; ++u) q[u] = src[(int64_t)(c + u) * S.stride];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) p16[u] += q[16 * r + u];
+    }
+    for (; c + 32 <= S.chunks; c += 32) {  // two rounds' loads in flight at once, added in the same order
+      float q[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) q[u] = src[(int64_t)(c + u) * S.stride];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p16[u] += q[u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p16[u] += q[16 + u];
+    }
     for (; c + 16 <= S.chunks; c += 16) {
       float q[16];
 #pragma unroll
