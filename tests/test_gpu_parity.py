@@ -529,3 +529,57 @@ def test_rejected_calls_leave_the_context_intact():
         assert torch.equal(x, y)
     env.close()
     twin.close()
+
+
+def _digest_torch(res):
+    """Order-sensitive 64-bit digest of a step's obs / reward / done / info (wrapping int64 arithmetic)."""
+    tot = torch.zeros((), dtype=torch.int64, device="cuda:0")
+    for t in (res.obs, res.reward, res.done, res.info):
+        bits = (t.view(torch.int32) if t.dtype == torch.float32 else t.to(torch.int32)).reshape(-1).to(torch.int64)
+        w = (torch.arange(bits.numel(), device="cuda:0", dtype=torch.int64) * 2654435761 + 1) % (1 << 31)
+        tot = tot * 1000003 + (bits * w).sum()
+    return int(tot.item())
+
+
+def _digest_np(out):
+    tot = np.int64(0)
+    with np.errstate(over="ignore"):
+        for k in ("obs", "reward", "done", "info"):
+            a = out[k]
+            bits = (a.view(np.int32) if a.dtype == np.float32 else a.astype(np.int32)).reshape(-1).astype(np.int64)
+            w = (np.arange(bits.size, dtype=np.int64) * 2654435761 + 1) % (1 << 31)
+            tot = tot * np.int64(1000003) + (bits * w).sum(dtype=np.int64)
+    return int(tot)
+
+
+def test_benchmarked_trajectories_bit_exact_at_full_size(oracle):
+    """bench.py's own workload at its own size -- 65 536 arenas, strong vs strong fused, auto-reset, seed 0,
+    env.reset(), the 1 000-step pre-roll as hk_rollout launches without outputs, then 500 hk_step launches with
+    obs / reward / done / info -- against the oracle's batched context stepped alongside: every step's outputs
+    equal (a 64-bit digest of all 65 536 rows per step, the full arrays at the last step), and the final state,
+    phases and counters equal.  The throughput figure is measured on exactly these trajectories."""
+    import bench
+
+    n, pre, steps = 65536, 1000, 500
+    env = _vec(n, policies=("strong", "strong"), auto_reset=True, seed=0)
+    env.reset()
+    ov = oracle.OracleVec(n, policies=("strong", "strong"), auto_reset=True, seed=0)
+    ov.reset(one_starts=env.one_starts.astype(np.uint8))
+    bench.preroll(env, pre, N)
+    for _ in range(pre):
+        ov.step()
+    for t in range(steps):
+        res = env.step()
+        want = ov.step()
+        assert _digest_torch(res) == _digest_np(want), f"step {pre + t}"
+    for k in ("obs", "reward", "done", "info"):
+        assert np.array_equal(_np(getattr(res, k)), want[k]), k
+    st, aux = env.get_state()
+    ost, oaux = ov.get_state()
+    assert np.array_equal(_np(st), ost) and np.array_equal(_np(aux), oaux)
+    assert np.array_equal(_np(env.opponent_phase()), ov.phase())
+    c, oc = env.counters(), ov.counters()
+    assert np.array_equal(c[:5], oc[:5]), (c[:7], oc[:7])
+    assert c[N.CNT_EPISODES] > n and c[N.CNT_TOI] > 0
+    env.close()
+    ov.close()
