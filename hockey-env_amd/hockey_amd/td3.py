@@ -418,7 +418,8 @@ def load_checkpoint(path):
     """A td3_*.pt (``torch.load(weights_only=True)``) or the ``<net>/<param>`` npz fixture of one
     (tests/golden/extract_resume_checkpoint.py) as the reference's {policy, critic, target_policy, target_critic}
     dict of CPU tensors."""
-    path = str(path)
+    import os
+    path = os.fsdecode(os.fspath(path))
     if path.endswith(".npz"):
         import numpy as np
         z = np.load(path)
