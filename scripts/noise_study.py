@@ -67,6 +67,11 @@ def config(protocol, noise, per=False, sp=False):
     common = dict(noise_mode=NOISES[noise], prioritized_replay=False, use_self_play=False, use_noise_annealing=True)
     if protocol == "scratch":
         return TD3Config(curriculum_name="noise_study", **common), None
+    if protocol == "stage1":
+        # definitions.py:70-90 stage1: from scratch, curriculum stage1 (the weak bot only), annealed noise (Gaussian
+        # there; --noise here), lr 4e-4, no PER, no self-play; compared with the reference's own loop
+        # (scripts/reference_loop_study.py --protocol stage1), the report has no multi-seed stage-1 table
+        return TD3Config(curriculum_name="stage1", lr_q=4e-4, lr_pol=4e-4, **common), None
     if protocol == "sp_per":
         # definitions.py:34-66 prioritized_selfplay_study: resume from weak_10k/td3_best.pt (= pretrained/stage_1 best,
         # pretrained/stage_2/config/run_info.json), curriculum "ablation" (= STAGE_2), OU noise, annealing, PER and
@@ -78,7 +83,7 @@ def config(protocol, noise, per=False, sp=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--protocol", choices=["scratch", "stage2", "sp_per"], required=True)
+    ap.add_argument("--protocol", choices=["scratch", "stage1", "stage2", "sp_per"], required=True)
     ap.add_argument("--per", type=int, default=0, help="sp_per: prioritized replay on (1) / off (0)")
     ap.add_argument("--sp", type=int, default=0, help="sp_per: self-play on (1) / off (0)")
     ap.add_argument("--noise", choices=sorted(NOISES), required=True)
@@ -97,7 +102,8 @@ def main():
     os.makedirs(args.out, exist_ok=True)
     name = f"{args.protocol}_{args.noise}" if args.protocol != "sp_per" else f"sp_per_p{args.per}_sp{args.sp}"
     stem = os.path.join(args.out, f"{name}_s{args.seed}")
-    ref = REFERENCE[args.noise] if args.protocol != "sp_per" else REFERENCE_SP_PER[(bool(args.per), bool(args.sp))]
+    ref = (REFERENCE_SP_PER[(bool(args.per), bool(args.sp))] if args.protocol == "sp_per"
+           else None if args.protocol == "stage1" else REFERENCE[args.noise])
     out = {"protocol": args.protocol, "noise": args.noise if args.protocol != "sp_per" else "ou", "seed": args.seed,
            "per": bool(cfg.prioritized_replay), "self_play": bool(cfg.use_self_play), "config": vars(cfg),
            "resume_from": None if resume is None else os.path.relpath(resume, ROOT), "arenas": n,

@@ -23,7 +23,7 @@ def load(dirs):
     for d in dirs:
         for f in sorted(glob.glob(os.path.join(d, "*_s*.json"))):
             r = json.load(open(f))
-            if "final_eval" not in r:
+            if "final_eval" not in r or r.get("reference") is None:  # stage1: no report table (reference_loop_compare.py)
                 continue
             label = r["noise"] if r["protocol"] != "sp_per" else f"per{int(r['per'])}_sp{int(r['self_play'])}"
             runs[(r["protocol"], label, r["seed"])] = r  # later directories override earlier partial runs

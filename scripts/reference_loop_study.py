@@ -113,11 +113,12 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--episodes", type=int, default=10_000)
     ap.add_argument("--curriculum", default="noise_study")
-    ap.add_argument("--protocol", choices=["scratch", "stage2", "sp_per"], default="scratch",
+    ap.add_argument("--protocol", choices=["scratch", "stage1", "stage2", "sp_per"], default="scratch",
                     help="stage2: the report's Stage II setup (definitions.py:93-114): resume from the stage-1 best "
                          "checkpoint, curriculum stage2, lr 3e-4, noise floor 0.06 (as scripts/noise_study.py); "
                          "sp_per: the baseline row of prioritized_selfplay_study (definitions.py:34-66): resume, "
-                         "curriculum ablation, OU noise, no PER, no self-play, config.py defaults otherwise")
+                         "curriculum ablation, OU noise, no PER, no self-play, config.py defaults otherwise; stage1: "
+                         "definitions.py:70-90, from scratch on the weak-bot curriculum")
     ap.add_argument("--final-games", type=int, default=1000)
     ap.add_argument("--episode-end", choices=["done", "max_steps"], default="done")
     ap.add_argument("--threads", type=int, default=1)
@@ -135,13 +136,15 @@ def main():
         over.update(curriculum_name="stage2", lr_q=3e-4, lr_pol=3e-4, noise_min_scale=0.06)
     if args.protocol == "sp_per":
         over.update(curriculum_name="ablation", noise_mode=NOISES["ou"])
+    if args.protocol == "stage1":  # definitions.py:70-90 (lr 4e-4 is config.py's default)
+        over.update(curriculum_name="stage1", lr_q=4e-4, lr_pol=4e-4)
     for k, v in over.items():
         setattr(cfg, k, v)
     train_env = OracleHockeyEnv()
     evaluators = {"strong": Evaluator(OracleHockeyOne(H, False), episodes=cfg.eval_episodes),
                   "weak": Evaluator(OracleHockeyOne(H, True), episodes=cfg.eval_episodes)}
     agent = TD3Agent(env=train_env, config=cfg, h=256, max_total_steps=args.episodes * cfg.max_steps, seed=args.seed)
-    if args.protocol != "scratch":  # agent.load (rl/td3/agent.py:278-286), read weights-only
+    if args.protocol not in ("scratch", "stage1"):  # agent.load (rl/td3/agent.py:278-286), read weights-only
         ck = torch.load(os.path.join(REF, "pretrained", "stage_1", "models", "td3_best.pt"), map_location="cpu",
                         weights_only=True)
         for key, net in (("policy", agent.policy), ("critic", agent.critic), ("target_policy", agent.target_policy),
