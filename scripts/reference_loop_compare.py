@@ -5,7 +5,7 @@ Inputs: runs of scripts/noise_study.py (the GPU loop, hockey_amd.td3.train) and 
 on 1 000 fresh placements per bot).  For each (protocol, noise) present in both: mean +- std (ddof 1) of the final
 win rates and returns of each loop, Welch's t between the loops with its two-sided p, the Mann-Whitney U p, and the
 mean evaluation score min(WR_strong, WR_weak) of each loop at every 1 000 episodes (the learning curve).  Win rates
-in percent.
+in percent.  Also the number of runs of each loop whose evaluations reach WR_weak >= 0.9, with Fisher's exact p.
 
 Usage: python scripts/reference_loop_compare.py --gpu profiles/r05/noise_runs --ref profiles/r05/reference_loop_stage2 \
            > profiles/r05/reference_loop_stage2_comparison.json
@@ -70,6 +70,12 @@ def main():
                          "welch_p": None if t is None else round(float(t.pvalue), 3),
                          "mann_whitney_p": round(float(stats.mannwhitneyu(a, b).pvalue), 3)}
         cell["score_curve"] = {"gpu": curve(g), "ref": curve(r)}
+        # runs whose evaluations reach WR_weak >= 0.9 at some point (the stage-1 "learned" mark), Fisher exact p
+        hit = lambda rs: sum(any(e["wr_weak"] >= 0.9 for e in x["evals"]) for x in rs)  # noqa: E731
+        hg, hr = hit(g), hit(r)
+        cell["reach_wr_weak_0.9"] = {"gpu": [hg, len(g)], "ref": [hr, len(r)],
+                                     "fisher_p": round(float(stats.fisher_exact([[hg, len(g) - hg],
+                                                                                [hr, len(r) - hr]]).pvalue), 3)}
         cell["best_episode"] = {"gpu": [x["best"]["episode"] for x in g], "ref": [x["best"]["episode"] for x in r]}
         out["cells"]["/".join(k)] = cell
     print(json.dumps(out, indent=1))
