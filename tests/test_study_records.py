@@ -30,7 +30,7 @@ def test_noise_study_summary_regenerates():
     assert got == want
 
 
-@pytest.mark.parametrize("ref", ["stage2", "sp_per", "scratch_ou"])
+@pytest.mark.parametrize("ref", ["stage1", "stage2", "sp_per", "scratch_ou"])
 def test_reference_loop_comparison_regenerates(ref):
     got = _run("reference_loop_compare.py", "--gpu", os.path.join("profiles", "r05", "noise_runs"),
                "--ref", os.path.join("profiles", "r05", f"reference_loop_{ref}"))
