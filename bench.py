@@ -15,10 +15,11 @@ Steady state: before the warmup every arena is pre-rolled --preroll steps (defau
 with no outputs, independent of --warmup), so the timed steps see desynchronised episodes at their steady
 contact / TOI load; the timed region must contain finished episodes (asserted).
 
-Output: ONE JSON line on rank 0 with `roofline` (step kernel, VALU-bound: active-lane VALU operations per
-launch from the committed rocprofv3 SQ counters / measured average kernel duration vs the fp32 VALU lane
-rate; `roofline.hbm`: algorithmic bytes / the same duration vs 8 TB/s) and `cpu_baseline` (the C oracle's
-batched context on the same workload on host cores, plus the C1 single-env number; rank 0 at N=1 only).
+Output: ONE JSON line on rank 0 with `roofline` (step kernel, VALU-bound: the algorithmic fp32 FLOPs of the
+workload per launch / measured average kernel duration vs the 157.3 TFLOP/s fp32 vector peak;
+`roofline.hbm`: algorithmic bytes / the same duration vs 8 TB/s; `roofline.valu_issue`: issued active-lane VALU
+operations from the committed SQ counters, reported beside, not as the headline) and `cpu_baseline` (the C
+oracle's batched context on the same workload on host cores, plus the C1 single-env number; rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -157,16 +158,34 @@ def preroll(env, steps, N):
         left -= k
 
 
-def reduce_over_ranks(elapsed, counters, dist, device):
-    """Whole-job numbers: the slowest rank's elapsed time (MAX) and the summed device counters (SUM).
-    The only collectives of the bench; none on the step path (arenas are sharded)."""
+def init_collectives(dist):
+    """The bench's process group: gloo over host tensors on the GPU path too.  Arenas are sharded with no
+    step-path exchange (north_star: "no RCCL collectives needed"), so the whole job needs only a
+    barrier, one MAX and one SUM of host scalars; RCCL is never brought up (tests/test_distributed_gloo.py
+    rehearses exactly this group)."""
+    dist.init_process_group(backend="gloo")
+    return dist.get_backend()
+
+
+def max_over_ranks(elapsed, dist):
+    """The slowest rank's elapsed time (MAX over a gloo group, host tensor)."""
     import torch
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    c = torch.tensor(counters, dtype=torch.int64, device=device)
+    return float(t.item())
+
+
+def reduce_over_ranks(elapsed, counters, dist, device=None):
+    """Whole-job numbers: the slowest rank's elapsed time (MAX) and the summed device counters (SUM), both on
+    host tensors over the gloo group.  The only collectives of the bench; none on the step path (arenas are
+    sharded).  `device` is accepted for old callers and ignored: nothing is reduced on the GPU."""
+    import numpy as np
+    import torch
+
+    c = torch.tensor(np.asarray(counters, dtype=np.int64), dtype=torch.int64)
     dist.all_reduce(c)
-    return float(t.item()), c.cpu().numpy()
+    return max_over_ranks(elapsed, dist), c.numpy()
 
 
 def shard_offset(rank, n_per_rank):
@@ -198,9 +217,7 @@ def _time_rollout(env, N, torch, dist, world, dev, args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dist)
     steps = launches * k
     return {"steps_per_launch": k, "launches": launches, "value": n * world * steps / elapsed,
             "unit": "env-steps/s", "ms_per_step": elapsed / steps * 1e3}
@@ -249,9 +266,7 @@ def _time_streams(args, N, torch, dist, world, rank, dev, pol):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dist)
     for e in envs:
         e.close()
     return {"streams": S, "arenas_per_stream": sizes, "hw_queues": q, "value": n * world * args.steps / elapsed,
@@ -442,10 +457,7 @@ def main():
 
     gpu = not args.rehearse
     if world > 1:
-        if gpu:
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend="gloo")
+        init_collectives(dist)  # gloo on the GPU path too: host scalars only, no RCCL bring-up
     if gpu:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -505,7 +517,7 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps if gpu else elapsed / args.steps * 1e3
     cnt = env.counters()
     if world > 1:
-        elapsed, cnt = reduce_over_ranks(elapsed, cnt, dist, dev)
+        elapsed, cnt = reduce_over_ranks(elapsed, cnt, dist)
     rollout = streams = None
     if gpu and args.rollout > 1:
         rollout = _time_rollout(env, N, torch, dist, world, dev, args)
@@ -551,26 +563,35 @@ def main():
                                    f"{'strong-vs-strong BasicOpponent on-GPU' if args.policy == 'basic' else 'random-vs-random'}"
                                    f", auto-reset", "arenas_per_gpu": n, "policy": args.policy,
                        "parallelism": f"arena-sharded x{world} (no collectives)"},
-            "roofline": {"bound": "valu", "achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
-                         "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
-                         "useful_frac": useful_tflops / FP32_PEAK_TFLOPS if useful_tflops else None,
-                         "useful": {"flops_per_env_step": flops, "achieved": useful_tflops, "peak": FP32_PEAK_TFLOPS,
-                                    "unit": "TFLOP/s", "from": "profiles/r04/flop_count.json (algorithmic FLOPs of "
-                                                              "Box2D's arithmetic, scripts/flop_count.py)"},
+            # the headline roof is ALGORITHMIC work: Box2D's useful fp32 FLOPs per env-step of this
+            # workload x arenas / the kernel's average launch duration, against the fp32 vector peak; the HBM roof
+            # (285 algorithmic B per env-step) beside it; issued active-lane VALU ops (what the SIMDs actually
+            # executed, from the committed SQ counters) under valu_issue, never as the headline
+            "roofline": {"bound": "valu", "achieved": useful_tflops, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": useful_tflops / FP32_PEAK_TFLOPS if useful_tflops else None,
+                         "basis": "algorithmic fp32 FLOPs of Box2D's arithmetic on this workload "
+                                  "(profiles/r04/flop_count.json, scripts/flop_count.py) per launch / kernel_avg_ms",
+                         "flops_per_env_step": flops,
                          "traffic": pmc.get("hbm_bytes_per_launch"),
                          "kernel": "hk::step_kernel", "kernel_avg_ms": kern_ms,
                          "kernel_avg_from": "HIP events bracketing the K timed launches on their stream: GPU time / K, "
                                             "launch gaps included",
-                         "valu_lane_ops_per_launch": lane_ops,
-                         "valu_issue_util": sq.get("valu_issue_util"), "valu_lane_util": sq.get("valu_lane_util"),
-                         "counters_from": sq.get("source"),
                          "library_hash": lib_hash, "source_hash": src_hash,
                          "counters_hash": {"sq": sq.get("source_hash"), "pmc": pmc.get("source_hash")},
                          "counters_stale": bool(stale),
                          "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": hbm_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": alg_bytes,
                                  "traffic_bytes_per_launch": pmc.get("hbm_bytes_per_launch"),
-                                 "traffic_from": pmc.get("source")}},
+                                 "traffic_from": pmc.get("source")},
+                         "valu_issue": {"achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+                                        "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
+                                        "lane_ops_per_launch": lane_ops,
+                                        "lane_ops_per_useful_flop": (lane_ops / (flops * n)
+                                                                     if lane_ops and flops else None),
+                                        "issue_util": sq.get("valu_issue_util"), "lane_util": sq.get("valu_lane_util"),
+                                        "counters_from": sq.get("source"),
+                                        "note": "issued active-lane VALU operations (SQ_THREAD_CYCLES_VALU), not "
+                                                "algorithmic work"}},
             "preroll": args.preroll,
             "episodes": int(cnt[N.CNT_EPISODES]),
             "toi_events": int(cnt[N.CNT_TOI]),

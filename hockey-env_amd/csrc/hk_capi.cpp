@@ -62,6 +62,9 @@ struct Ctx {
 // idle limit bounds what a resident server can cost other work: a kernel that lands on the server stream's hardware
 // queue (streams share the box's 4 queues) or a device-wide synchronise waits for its idle exit.
 constexpr int kSrvIdleMs = 4, kSrvLifeMs = 2000;
+// the longest a server-path hk_step_host call waits for its answer (the server is ordered after the caller's
+// stream, so this also bounds the work queued there before the step); then it fails with HK_E_DEVICE
+constexpr int kSrvWaitMs = 10000;
 
 // At most ONE resident step server per device and process: every single-arena context's server runs on
 // the device's one server stream, and a context that starts its server first stops the running one of another
@@ -375,12 +378,25 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
         c->srv_start = std::chrono::steady_clock::now();
       }
       // Spin on the completion word; every 4096 polls ask the server's stream, so a server that faulted returns
-      // its error and one that exited on its own before serving this request is replaced.
+      // its error and one that exited on its own before serving this request is replaced.  The wait is bounded
+      // (ADVICE r05): the slot's lock is held here, so a server that never starts (the caller's stream blocked
+      // on an event that never fires) must not hold every other facade on this device forever.  Past the deadline
+      // the request is withdrawn (the quit word: a server that starts later exits without serving it), the
+      // server stays recorded as running, so the next stop of this context waits for its stream, and the call
+      // fails with HK_E_DEVICE.
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(kSrvWaitMs);
       uint32_t k = 1;
       for (; *word != seq; ++k) {
         if ((k & 4095u) == 0u) {
           const hipError_t q = hipStreamQuery(slot.stream);
-          if (q == hipErrorNotReady) continue;
+          if (q == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() < deadline) continue;
+            std::atomic_thread_fence(std::memory_order_release);
+            *req_word(c) = hk::kServerQuit;
+            if (*word == seq) break;  // answered while the request was being withdrawn
+            return fail(HK_E_DEVICE, "hk_step_host: the step server did not answer within the wait limit "
+                                     "(is the calling stream blocked?)%s");
+          }
           if (q != hipSuccess) {
             c->srv_running = false;
             slot.owner = nullptr;

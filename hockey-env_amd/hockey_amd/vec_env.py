@@ -23,6 +23,11 @@ import torch
 
 from . import _native as N
 
+from .constants import Mode, parse_mode
+from .placement import np_random, placement
+
+# torch's private accessor for the current raw stream (no Stream object per call); the public form is the fallback,
+# and tests/test_gpu_facade.py holds the two equal inside and outside a torch.cuda.stream context
 _getraw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
@@ -31,8 +36,7 @@ def _raw_stream(index):
     if _getraw is not None:
         return _getraw(index)
     return torch.cuda.current_stream(index).cuda_stream
-from .constants import Mode, parse_mode
-from .placement import np_random, placement
+
 
 _POLICIES = {"external": N.POLICY_EXTERNAL, "random": N.POLICY_RANDOM, "weak": N.POLICY_BASIC_WEAK,
              "strong": N.POLICY_BASIC_STRONG}

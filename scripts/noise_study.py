@@ -81,6 +81,22 @@ def config(protocol, noise, per=False, sp=False):
     return TD3Config(curriculum_name="stage2", lr_q=3e-4, lr_pol=3e-4, noise_min_scale=0.06, **common), RESUME
 
 
+# episodes of each protocol's Experiment in rl/experiment/definitions.py (noise study :16-18, PER / self-play
+# study :53-55, stage1 :72-74, stage2 :97-99)
+DEFINITION_EPISODES = {"scratch": 10_000, "sp_per": 10_000, "stage1": 10_000, "stage2": 15_000}
+
+
+def deviations(protocol, episodes):
+    """Explicit deviations of this run from the reference's Experiment definition (recorded in the run
+    JSON, not only in a docstring)."""
+    want = DEFINITION_EPISODES[protocol]
+    if episodes == want:
+        return []
+    return [{"what": "noise-study length", "episodes": episodes, "definition_episodes": want,
+             "why": "the report's Stage II table is compared at the noise study's 10 000 episodes; pass --episodes "
+                    f"{want} for the definition's length"}]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--protocol", choices=["scratch", "stage1", "stage2", "sp_per"], required=True)
@@ -107,7 +123,8 @@ def main():
     out = {"protocol": args.protocol, "noise": args.noise if args.protocol != "sp_per" else "ou", "seed": args.seed,
            "per": bool(cfg.prioritized_replay), "self_play": bool(cfg.use_self_play), "config": vars(cfg),
            "resume_from": None if resume is None else os.path.relpath(resume, ROOT), "arenas": n,
-           "episodes": rounds * n, "eval_episodes": args.eval_episodes, "reference": ref, "evals": [], "best": None}
+           "episodes": rounds * n, "eval_episodes": args.eval_episodes, "reference": ref, "evals": [], "best": None,
+           "deviations": deviations(args.protocol, rounds * n)}
     t0 = time.time()
     best = {"score": float("-inf")}
 

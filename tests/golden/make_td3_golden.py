@@ -24,21 +24,16 @@ import torch
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(OUT))
-sys.path[:0] = [REF, os.path.join(ROOT, "hockey-env_amd")]
+sys.path[:0] = [REF, OUT, os.path.join(ROOT, "hockey-env_amd")]
 
 from hockey_amd.td3 import TD3, TD3Config  # noqa: E402
 
-H, B, K = 32, 64, 30
+from g9_batches import B, H, K  # noqa: E402
+from g9_batches import batch as _batch  # noqa: E402
 
 
 def batch(k):
-    g = torch.Generator().manual_seed(1000 + k)
-    s = torch.randn(B, 18, generator=g)
-    a = torch.rand(B, 4, generator=g) * 2 - 1
-    r = torch.randn(B, generator=g) * 3
-    s2 = torch.randn(B, 18, generator=g)
-    d = (torch.rand(B, generator=g) < 0.15).float()
-    return s, a, r, s2, d
+    return _batch(k, B)
 
 
 def main(h=H, b=B, k_updates=K, out_name="g9_td3_learner.npz"):

@@ -114,3 +114,51 @@ def test_bench_hung_rank_times_out_and_fails_the_launch():
     assert rc != 0 and not lines
     assert "still running after 20 s" in err, err[-2000:]
     assert time.monotonic() - t0 < 120
+
+
+def test_bench_never_constructs_an_nccl_group(monkeypatch):
+    """the multi-GPU bench needs a barrier, a MAX and a SUM of host scalars, so its GPU path
+    brings up the same gloo group this file rehearses, never RCCL.  Statically: the only init_process_group call
+    in bench.py is init_collectives' gloo one and no string names nccl; dynamically: init_collectives asks for
+    gloo, and reduce_over_ranks reduces host tensors only."""
+    import ast
+    import sys
+
+    import torch
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "bench.py")).read()
+    tree = ast.parse(src)
+    calls = [n for n in ast.walk(tree) if isinstance(n, ast.Call) and getattr(n.func, "attr", "") == "init_process_group"]
+    assert len(calls) == 1
+    kw = {k.arg: k.value.value for k in calls[0].keywords if isinstance(k.value, ast.Constant)}
+    assert kw == {"backend": "gloo"}
+    consts = [n.value.lower() for n in ast.walk(tree) if isinstance(n, ast.Constant) and isinstance(n.value, str)]
+    assert not any("nccl" in c for c in consts)
+    assert "device_id" not in src
+
+    sys.path.insert(0, root)
+    import bench
+
+    seen = {}
+
+    class FakeDist:
+        class ReduceOp:
+            MAX = "max"
+
+        @staticmethod
+        def init_process_group(backend=None, **kw):
+            seen["backend"] = backend
+
+        @staticmethod
+        def get_backend():
+            return seen["backend"]
+
+        @staticmethod
+        def all_reduce(t, op=None):
+            seen.setdefault("devices", []).append(t.device.type)
+
+    assert bench.init_collectives(FakeDist) == "gloo"
+    el, c = bench.reduce_over_ranks(1.5, np.arange(4), FakeDist)
+    assert el == 1.5 and list(c) == [0, 1, 2, 3]
+    assert seen["devices"] == ["cpu", "cpu"]

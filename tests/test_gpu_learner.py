@@ -28,7 +28,7 @@ LOSS_RTOL, PARAM_ATOL = 1e-4, 1e-5
 
 def _golden_batches():
     sys.path.insert(0, GOLDEN)
-    import make_td3_golden as M
+    import g9_batches as M
     return M
 
 
@@ -82,8 +82,7 @@ def test_fused_learner_matches_reference_learner_g9b():
     M = _golden_batches()
     g = np.load(os.path.join(GOLDEN, "g9b_td3_learner_h256.npz"))
     B, K = int(g["b"]), len(g["critic_loss"])
-    M.B = B
-    batches = [M.batch(k) for k in range(K)]
+    batches = [M.batch(k, B) for k in range(K)]
     agent = TD3(TD3Config(), device=DEV, seed=0, h=256)
     init = TD3(TD3Config(), device="cpu", seed=0, h=256)  # the golden's initial weights (CPU init of seed 0)
     for src, dst in ((init.actor, agent.actor), (init.critic, agent.critic), (init.target_actor, agent.target_actor),

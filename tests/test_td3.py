@@ -31,7 +31,7 @@ def test_learner_matches_reference_learner_g9():
     import sys
 
     sys.path.insert(0, GOLDEN)
-    from make_td3_golden import B, H, K, batch
+    from g9_batches import B, H, K, batch
 
     g9 = np.load(os.path.join(GOLDEN, "g9_td3_learner.npz"))
     agent = TD3(TD3Config(), device="cpu", seed=0, h=H)
@@ -428,14 +428,14 @@ def test_learner_matches_reference_learner_g9b_wide():
     import sys
 
     sys.path.insert(0, GOLDEN)
-    import make_td3_golden as M
+    import g9_batches as M
 
     g = np.load(os.path.join(GOLDEN, "g9b_td3_learner_h256.npz"))
-    M.B = int(g["b"])
+    gb = int(g["b"])
     agent = TD3(TD3Config(), device="cpu", seed=0, h=int(g["h"]))
     for k in range(len(g["critic_loss"])):
         torch.manual_seed(2000 + k)
-        al, cl = agent.update(*M.batch(k))
+        al, cl = agent.update(*M.batch(k, gb))
         assert abs(float(cl) - g["critic_loss"][k]) <= 1e-5 * max(1.0, abs(g["critic_loss"][k])), k
         if al is not None:
             assert abs(float(al) - g["actor_loss"][k]) <= 1e-5 * max(1.0, abs(g["actor_loss"][k])), k
@@ -443,4 +443,3 @@ def test_learner_matches_reference_learner_g9b_wide():
                       ("target_critic", agent.target_critic)):
         for key, v in net.state_dict().items():
             np.testing.assert_allclose(v.numpy(), g[f"{name}/{key}"], rtol=0, atol=1e-6, err_msg=f"{name}/{key}")
-    M.B = 64
