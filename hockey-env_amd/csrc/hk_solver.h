@@ -676,6 +676,73 @@ HK_DEV void vtwo_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool sep, bo
 #pragma unroll
   for (int k = 0; k < 20; ++k) t.sn[k] = sn[k];
 }
+// The tail's two-contact shape (r06, scripts/tail_shape_study.c: ~90 % of the two-contact family's iterations from
+// iteration 56 on): one island whose contact 1 has a static body A and contact 0's body A as its body B (b1 == a0:
+// player-puck, then wall-player), optionally with one-contact lanes riding along.  The shared body has ONE home
+// (contact 0's A locals): contact 1 reads it directly and its update is committed back with one select per component
+// (riders discard theirs), instead of the generic chunk's per-lane refresh selects after both contacts and its
+// exec-mask guard on contact 1; contact 1 runs the static-body-A row.  Riders (two == false) compute a dummy contact
+// 1 on their own slot 1, whose impulses are restored at the chunk's end (that slot may hold another island's retired
+// contact); their snapshot words of contact 1 are 0, as in the generic chunk.  Every S2 lane's float operations are
+// the generic chunk's, in its order, so the result is bit-identical; the snapshot words keep their meaning (contact
+// 1's body B words are the shared body's, contact 1's static body A words are 0), so the chain carries across.
+template <int kP0, int kP1>
+HK_DEV void vtwo_s2_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s2, bool dA0, uint32_t mA0, int &it,
+                          int stop, int first, bool &active, bool &on0, bool &on1) {
+  f2 vA0 = t.vA0, vB0 = t.vB0;
+  float wA0 = t.wA0, wB0 = t.wB0;
+  uint32_t sn[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) sn[k] = t.sn[k];
+  const float ni0 = s1.ni[0], ni1 = s1.ni[1], ti0 = s1.ti[0], ti1 = s1.ti[1];
+  HK_MARK(vtwo_s2_begin);
+  for (; it < stop && active; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vA0 = f2{mask_f(vA0[0], mA0), mask_f(vA0[1], mA0)};  // a rider's static A: +0 (lane_mask)
+      wA0 = mask_f(wA0, mA0);
+      fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
+      f2 vA1 = f2{0.0f, 0.0f}, vB1 = vA0;
+      float wA1 = 0.0f, wB1 = wA0;
+      fslot_solve_velocity_p<true, kP1>(s1, vA1, wA1, vB1, wB1);
+      vA0 = sel2(two, vB1, vA0);
+      wA0 = two ? wB1 : wA0;
+    }
+    const uint32_t x[20] = {__float_as_uint(vB0[0]), __float_as_uint(vB0[1]), __float_as_uint(wB0),
+                            dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
+                            dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
+                            __float_as_uint(s0.ti[0]), __float_as_uint(s0.ti[1]),
+                            two ? __float_as_uint(vA0[0]) : 0u, two ? __float_as_uint(vA0[1]) : 0u,
+                            two ? __float_as_uint(wA0) : 0u, 0u, 0u, 0u,
+                            two ? __float_as_uint(s1.ni[0]) : 0u, two ? __float_as_uint(s1.ni[1]) : 0u,
+                            two ? __float_as_uint(s1.ti[0]) : 0u, two ? __float_as_uint(s1.ti[1]) : 0u};
+    uint32_t d = 0u;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+      d |= x[k] ^ sn[k];
+      sn[k] = x[k];
+    }
+    if (it + 3 >= first && d == 0u) {  // no lane here is split over two islands (see the dispatch)
+      on0 = false;
+      on1 = false;
+      active = false;
+    }
+  }
+  HK_MARK(vtwo_s2_end);
+  if (it >= kVelIters) active = false;
+  t.vA0 = vA0; t.vB0 = vB0; t.wA0 = wA0; t.wB0 = wB0;
+  // the generic chunks' copy of the shared body, for S2 lanes only: a lane of another shape that finished in an
+  // earlier chunk runs this code too (exec is not masked here) and its copies must stay as they are
+  t.vB1 = sel2(s2, vA0, t.vB1);
+  t.wB1 = s2 ? wA0 : t.wB1;
+  s1.ni[0] = two ? s1.ni[0] : ni0;
+  s1.ni[1] = two ? s1.ni[1] : ni1;
+  s1.ti[0] = two ? s1.ti[0] : ti0;
+  s1.ti[1] = two ? s1.ti[1] : ti1;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) t.sn[k] = sn[k];
+}
+
 // runs until every lane is done or no running lane has both contacts live (then the one-contact family takes
 // over).  on0 / on1 in: the lane's contacts that iterate (on1 == two); out: the ones still unfinished.
 HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &active, int first, bool &on0,
@@ -700,9 +767,23 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
   t.vB1 = F2(q);
 #pragma unroll
   for (int k = 0; k < 20; ++k) t.sn[k] = 0u;
+  // the S2 shape (see vtwo_s2_chunk): one island, contact 1's body A static and its body B contact 0's body A
+  const bool s2 = two && !sep && !dA1 && b1a0;
   while (wave_any(active) && wave_any(active && on0 && on1)) {
     const int stop = chunk_end(it);
-    if (wave_any(active && !on0))
+    // S2 chunk: every running lane is an S2 lane with both contacts live, or a one-contact rider (two == false)
+    const bool s2ok = !wave_any(active && (!on0 || (two && !(s2 && on1))));
+    if (s2ok && !wave_any(active && two && vc1 != 1)) {
+      if (!wave_any(active && vc0 != 1))
+        vtwo_s2_chunk<1, 1>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
+      else
+        vtwo_s2_chunk<0, 1>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
+    } else if (s2ok && !wave_any(active && two && vc1 != 2)) {
+      if (!wave_any(active && vc0 != 1))
+        vtwo_s2_chunk<1, 2>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
+      else
+        vtwo_s2_chunk<0, 2>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
+    } else if (wave_any(active && !on0))
       vtwo_chunk<0, 0, true>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                              on1);
     else if (!wave_any(active && (vc0 != 1 || vc1 != 1)))

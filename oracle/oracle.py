@@ -142,6 +142,9 @@ class OracleWorld:
 VAR_REVERSE, VAR_NO_BLOCK, VAR_NO_SLEEP, VAR_ITERS_8_3 = 1, 2, 4, 8
 # deliberately wrong physics: negative controls of the behavioural pins (scripts/pin_power_study.py)
 VAR_REST_THRESH0, VAR_ARITH_FRIC, VAR_NO_TOI, VAR_REST_MIN = 16, 32, 64, 128
+# goal-path variants (hk_oracle.c HKO_VAR_SENSOR_* / HKO_VAR_KEEP_COM)
+VAR_SENSOR_SKIN_PLUS, VAR_SENSOR_SKIN_MINUS, VAR_SENSOR_SWEPT, VAR_KEEP_COM = 256, 512, 1024, 2048
+VAR_SENSOR_CORE = 4096
 
 
 def set_variant(flags):

@@ -1,0 +1,201 @@
+/* Which island shapes run a wave's velocity tail? (analysis tool, not product code; r06)
+ *
+ * Builds the CPU oracle with hooks on every island velocity iteration (HKO_VEL_HOOK) and on the arena being
+ * stepped (HKO_ARENA_HOOK), runs the bench workload (strong-vs-strong, NORMAL, auto-reset, Philox streams), and
+ * records per arena and step its island solves: contact count, the kernel's period-4 exit iteration, and the
+ * island's shape (per contact: body A / body B as island-body indices, body A dynamic or static, point count).
+ * It then replays the kernel's velocity-family dispatch (hk_solver.h velocity_iterations) over waves of 64
+ * consecutive arenas: at every chunk start (iterations 0, 8, 16, 24, 56, 88, 120, 152) the running lanes, their
+ * live contact counts and shapes, and so which family the wave runs and whether its running multi-contact lanes
+ * share one shape.  Weighted by the chunk's iterations, this says how much of the velocity tail a shape-specialised
+ * family (shared bodies aliased at compile time, no refresh selects) could run.
+ *
+ *   gcc -O2 -fopenmp -ffp-contract=off -o /tmp/tail_shape scripts/tail_shape_study.c -lm && /tmp/tail_shape 16384 300 60
+ */
+#define HKO_VEL_HOOK(S, Vl, nb, it, toi) ts_hook((const void *)(S), (const void *)(Vl), (nb), (it), (toi))
+static void ts_hook(const void *S, const void *Vl, int nb, int it, int toi);
+#define HKO_ARENA_HOOK(i) ts_arena(i)
+#include <stdint.h>
+static void ts_arena(int64_t i);
+#include <stdio.h>
+#include "../oracle/hk_oracle.c"
+
+#define MAXW 96
+#define MAXSOLVE 4
+typedef struct {
+  int n, cur;
+  int iA[4], iB[4], dynA[4], cnt[4];
+} solve_rec;
+typedef struct {
+  int ns;
+  solve_rec s[MAXSOLVE];
+} arena_rec;
+
+static __thread uint32_t g_x[VEL_ITERS][MAXW];
+static __thread int64_t g_arena = -1;
+static arena_rec *g_rec;
+static int g_on;
+
+static void ts_arena(int64_t i) { g_arena = i; }
+
+static void ts_hook(const void *Sv, const void *Vlv, int nb, int it, int toi) {
+  const csolver *S = (const csolver *)Sv;
+  const velv *Vl = (const velv *)Vlv;
+  int n = 0;
+  uint32_t *x = g_x[it];
+  for (int i = 0; i < nb && n + 3 <= MAXW; ++i) {
+    memcpy(&x[n++], &Vl[i].v.x, 4);
+    memcpy(&x[n++], &Vl[i].v.y, 4);
+    memcpy(&x[n++], &Vl[i].w, 4);
+  }
+  for (int i = 0; i < S->n; ++i)
+    for (int j = 0; j < S->vc[i].count && n + 2 <= MAXW; ++j) {
+      memcpy(&x[n++], &S->vc[i].p[j].ni, 4);
+      memcpy(&x[n++], &S->vc[i].p[j].ti, 4);
+    }
+  if (it != VEL_ITERS - 1 || !g_on || toi || g_arena < 0) return;
+  int cur = VEL_ITERS;
+  for (int k = 7; k < VEL_ITERS; k += 4)
+    if (!memcmp(g_x[k], g_x[k - 4], 4 * n)) { cur = k + 1; break; }
+  arena_rec *r = &g_rec[g_arena];
+  if (r->ns >= MAXSOLVE) return;
+  solve_rec *s = &r->s[r->ns++];
+  s->n = S->n;
+  s->cur = cur;
+  for (int i = 0; i < 4; ++i) {
+    const int on = i < S->n;
+    s->iA[i] = on ? S->vc[i].iA : -1;
+    s->iB[i] = on ? S->vc[i].iB : -1;
+    s->dynA[i] = on ? S->vc[i].mA != 0.0f : 0;
+    s->cnt[i] = on ? S->vc[i].count : 0;
+  }
+}
+
+/* shape key of a lane's live contacts (islands in solve order, contacts in island order): per contact
+ * "A<idx|s>B<idx>p<count>", body indices renumbered in first-appearance order across the lane */
+static void shape_key(const arena_rec *r, int t, char *out, int *live) {
+  int map[16][8];
+  for (int a = 0; a < 16; ++a)
+    for (int b = 0; b < 8; ++b) map[a][b] = -1;
+  int next = 0, L = 0;
+  out[0] = 0;
+  for (int k = 0; k < r->ns; ++k) {
+    const solve_rec *s = &r->s[k];
+    if (s->cur <= t) continue;
+    for (int i = 0; i < s->n && i < 4; ++i) {
+      int a = -1, b;
+      if (s->dynA[i]) {
+        if (map[k][s->iA[i]] < 0) map[k][s->iA[i]] = next++;
+        a = map[k][s->iA[i]];
+      }
+      if (map[k][s->iB[i]] < 0) map[k][s->iB[i]] = next++;
+      b = map[k][s->iB[i]];
+      char buf[32];
+      if (a < 0) snprintf(buf, sizeof buf, "[s%dp%d]", b, s->cnt[i]);
+      else snprintf(buf, sizeof buf, "[%d%dp%d]", a, b, s->cnt[i]);
+      strcat(out, buf);
+      ++L;
+    }
+  }
+  *live = L;
+}
+
+#define NKEY 4096
+static char keys[NKEY][64];
+static double key_w[3][NKEY];
+static int nkeys;
+static double gen_mix[2][2];
+static int key_id(const char *k) {
+  for (int i = 0; i < nkeys; ++i)
+    if (!strcmp(keys[i], k)) return i;
+  if (nkeys < NKEY) { strcpy(keys[nkeys], k); return nkeys++; }
+  return NKEY - 1;
+}
+
+int main(int argc, char **argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 16384, pre = argc > 2 ? atoi(argv[2]) : 300,
+            steps = argc > 3 ? atoi(argv[3]) : 60;
+  const int32_t cfg[6] = {1, 0, 1, 0, 3, 3}; /* keep_mode, NORMAL, auto-reset, copy, strong, strong */
+  hkov *v = hkov_create(n, cfg, 1234, 0);
+  hkov_time_steps(v, pre, 0);
+  g_rec = (arena_rec *)calloc(n, sizeof(arena_rec));
+  const int starts[9] = {0, 8, 16, 24, 56, 88, 120, 152, 180};
+  /* per family (0 one, 1 two, 2 general): iterations x waves where the chunk's running lanes all share one
+   * multi-contact shape ("uniform") or not; and the shape histogram of uniform chunks */
+  double fam_it[3] = {0, 0, 0}, uni_it[3] = {0, 0, 0}, mixed_only_one[3] = {0, 0, 0};
+  double tail_fam[3] = {0, 0, 0}, tail_uni[3] = {0, 0, 0};
+  int64_t waves = 0;
+  for (int st = 0; st < steps; ++st) {
+    memset(g_rec, 0, n * sizeof(arena_rec));
+    g_on = 1;
+    hkov_step(v, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
+    g_on = 0;
+    for (int w0 = 0; w0 + 64 <= n; w0 += 64) {
+      ++waves;
+      /* the wave's last chunk with a running lane: the chunk that ends the wave's velocity phase */
+      int last_c = -1;
+      for (int c = 0; c < 8; ++c)
+        for (int l = 0; l < 64; ++l)
+          for (int k = 0; k < g_rec[w0 + l].ns; ++k)
+            if (g_rec[w0 + l].s[k].cur > starts[c]) last_c = c;
+      for (int c = 0; c < 8; ++c) {
+        const int t = starts[c], len = starts[c + 1] - starts[c];
+        int maxlive = 0, nmulti = 0, multi_key = -1, uniform = 1, anyone = 0;
+        for (int l = 0; l < 64; ++l) {
+          char key[64];
+          int live;
+          shape_key(&g_rec[w0 + l], t, key, &live);
+          if (!live) continue;
+          if (live > maxlive) maxlive = live;
+          if (live == 1) { anyone = 1; continue; }
+          const int id = key_id(key);
+          if (multi_key < 0) multi_key = id;
+          else if (multi_key != id) uniform = 0;
+          ++nmulti;
+        }
+        if (!maxlive) continue;
+        const int fam = maxlive > 2 ? 2 : maxlive - 1;
+        fam_it[fam] += len;
+        /* uniform: every running multi-contact lane has the same shape and no one-contact lane rides along */
+        const int uni = fam == 0 || (uniform && !anyone);
+        if (uni) uni_it[fam] += len;
+        if (fam > 0 && uniform && anyone) mixed_only_one[fam] += len;
+        if (c >= 4) {
+          tail_fam[fam] += len;
+          if (uni) tail_uni[fam] += len;
+        }
+        if (fam > 0 && uniform && multi_key >= 0 && c >= 4) key_w[anyone ? 1 : 0][multi_key] += len;
+        if (c == last_c && fam > 0 && multi_key >= 0) key_w[2][multi_key] += 1;
+        if (fam == 2 && c >= 4) { /* general-family tail chunks: the live-contact counts of the running lanes */
+          int cnt[5] = {0, 0, 0, 0, 0};
+          for (int l = 0; l < 64; ++l) {
+            char key[64];
+            int live;
+            shape_key(&g_rec[w0 + l], t, key, &live);
+            if (live) ++cnt[live > 4 ? 4 : live];
+          }
+          gen_mix[cnt[1] > 0][cnt[2] > 0] += len;
+        }
+      }
+    }
+  }
+  printf("%d arenas x %d steps after %d (%lld waves)\n", n, steps, pre, (long long)waves);
+  const char *fn[3] = {"one", "two", "general"};
+  for (int f = 0; f < 3; ++f)
+    printf("family %-8s iterations per wave %.2f; all running multi-contact lanes one shape, no rider: %.1f%%; "
+           "one shape + one-contact riders: %.1f%% | chunks from it 56: %.2f per wave, uniform %.1f%%\n",
+           fn[f], fam_it[f] / waves, fam_it[f] ? 100 * uni_it[f] / fam_it[f] : 0,
+           fam_it[f] ? 100 * mixed_only_one[f] / fam_it[f] : 0, tail_fam[f] / waves,
+           tail_fam[f] ? 100 * tail_uni[f] / tail_fam[f] : 0);
+  printf("shapes of uniform tail chunks (it >= 56), iterations per 1000 waves: [no riders] [with one-contact riders]"
+         " | waves whose last chunk has this shape among its multi-contact lanes\n");
+  for (int i = 0; i < nkeys; ++i)
+    if (key_w[0][i] + key_w[1][i] >= 0.002 * waves || key_w[2][i] >= 0.001 * waves)
+      printf("  %-40s %9.1f %9.1f | %7.0f\n", keys[i], 1000 * key_w[0][i] / waves, 1000 * key_w[1][i] / waves,
+             key_w[2][i]);
+  printf("general-family tail iterations per 1000 waves by rider kinds: alone %.1f, +1-contact %.1f, +2-contact "
+         "%.1f, +both %.1f\n", 1000 * gen_mix[0][0] / waves, 1000 * gen_mix[1][0] / waves, 1000 * gen_mix[0][1] / waves,
+         1000 * gen_mix[1][1] / waves);
+  hkov_destroy(v);
+  return 0;
+}
