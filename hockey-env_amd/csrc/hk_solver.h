@@ -13,7 +13,8 @@ namespace hk {
 
 // Host harness only (hostcheck, HK_HOST_DIAG): how often the velocity loop's island retirement and slot swaps
 // ran, so a CPU test can show that its lockstep runs exercised them.  [0] an island retired while another
-// of its lane's islands kept iterating, [1] a lane's live contacts were swapped into slots 0/1.
+// of its lane's islands kept iterating, [1] a lane's live contacts were swapped into slots 0/1, [2] an S3 lane
+// entered the three-contact shape family, [3] an S2 lane ran a two-contact shape chunk.
 #ifdef HK_HOST_DIAG
 extern unsigned long long g_hk_host_diag[4];
 #define HK_HOST_DIAG_INC(k) (++g_hk_host_diag[k])
@@ -694,6 +695,7 @@ HK_DEV void vtwo_s2_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s2, 
   uint32_t sn[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) sn[k] = t.sn[k];
+  if (active && two) HK_HOST_DIAG_INC(3);
   const float ni0 = s1.ni[0], ni1 = s1.ni[1], ti0 = s1.ti[0], ti1 = s1.ti[1];
   HK_MARK(vtwo_s2_begin);
   for (; it < stop && active; it += 4) {
@@ -814,6 +816,100 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
   }
 }
 
+// The tail's three-contact shape (r06, scripts/tail_shape_study.c): one island of three one-point contacts, slot 0
+// = (static, X), slot 1 = (Y, X), slot 2 = (static, Y) -- wall-puck, player-puck, wall-player -- optionally with
+// one-contact lanes riding along (their contact swapped into slot 0).  X and Y live in locals, aliased at compile
+// time, instead of the general family's body-file gathers and scatters (~30 selects per contact): slot 0 runs the
+// generic row on (A0, X) (a rider's own bodies; an S3 lane's A0 is static, +0), slot 1 the dynamic row on (Y, X),
+// whose update of X a rider discards (one select per component; its Y is a dummy never written back), slot 2 the
+// static-body-A row on Y.  Riders' slot 1 / 2 impulses are restored at the end (another island's retired contacts
+// may sit there).  The snapshot covers X, Y, A0 and the three contacts' impulses (a rider: its own body pair and
+// impulses), the island's whole state, so the periodic exit stays exact; this family starts its own chain.  Each S3
+// lane's float operations are the general family's, in its order.  Runs while some S3 lane iterates.
+template <int kP0>
+HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, uint32_t mA0, bool dA0, f2 &vA0, float &wA0,
+                            f2 &vX, float &wX, f2 &vY, float &wY, uint32_t (&sn)[17], int &it, int stop, int first,
+                            bool &active) {
+  HK_MARK(vthree_begin);
+  for (; it < stop && active; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vA0 = f2{mask_f(vA0[0], mA0), mask_f(vA0[1], mA0)};  // static A (every S3 lane, static riders): +0
+      wA0 = mask_f(wA0, mA0);
+      fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vX, wX);
+      f2 vB1 = vX;
+      float wB1 = wX;
+      fslot_solve_velocity_p<false, 1>(s1, vY, wY, vB1, wB1);
+      vX = sel2(s3, vB1, vX);
+      wX = s3 ? wB1 : wX;
+      f2 vA2 = f2{0.0f, 0.0f};
+      float wA2 = 0.0f;
+      fslot_solve_velocity_p<true, 1>(s2, vA2, wA2, vY, wY);
+    }
+    const uint32_t x[17] = {__float_as_uint(vX[0]), __float_as_uint(vX[1]), __float_as_uint(wX),
+                            dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
+                            dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
+                            __float_as_uint(s0.ti[0]), __float_as_uint(s0.ti[1]),
+                            s3 ? __float_as_uint(vY[0]) : 0u, s3 ? __float_as_uint(vY[1]) : 0u,
+                            s3 ? __float_as_uint(wY) : 0u, s3 ? __float_as_uint(s1.ni[0]) : 0u,
+                            s3 ? __float_as_uint(s1.ti[0]) : 0u, s3 ? __float_as_uint(s2.ni[0]) : 0u,
+                            s3 ? __float_as_uint(s2.ti[0]) : 0u};
+    uint32_t d = 0u;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+      d |= x[k] ^ sn[k];
+      sn[k] = x[k];
+    }
+    if (it + 3 >= first && d == 0u) active = false;
+  }
+  HK_MARK(vthree_end);
+  if (it >= kVelIters) active = false;
+}
+HK_DEV bool s3_shape(const FSlot &s0, const FSlot &s1, const FSlot &s2) {
+  return fs_bA(s0) >= 3 && fs_bA(s2) >= 3 && fs_bA(s1) < 3 && fs_bB(s0) == fs_bB(s1) && fs_bA(s1) == fs_bB(s2) &&
+         fs_vcount(s0) == 1 && fs_vcount(s1) == 1 && fs_vcount(s2) == 1;
+}
+// s3: this lane is an S3 lane (else a one-contact rider with its contact in slot 0)
+HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, int &it, bool &active, int first) {
+  const bool entered = active;
+  const int a0 = fs_bA(s0), x = fs_bB(s0), y = s3 ? fs_bA(s1) : x;
+  const bool dA0 = a0 < 3;
+  const uint32_t mA0 = lane_mask(dA0);
+  const int vc0 = fs_vcount(s0);
+  v2 q;
+  float wA0, wX, wY;
+  get_vel_a(B, a0, q, wA0);
+  f2 vA0 = F2(q);
+  get_vel_b(B, x, q, wX);
+  f2 vX = F2(q);
+  get_vel_b(B, y, q, wY);
+  f2 vY = F2(q);
+  const float ni1[2] = {s1.ni[0], s1.ni[1]}, ti1[2] = {s1.ti[0], s1.ti[1]};
+  const float ni2[2] = {s2.ni[0], s2.ni[1]}, ti2[2] = {s2.ti[0], s2.ti[1]};
+  uint32_t sn[17];
+#pragma unroll
+  for (int k = 0; k < 17; ++k) sn[k] = 0u;
+  while (wave_any(active && s3)) {
+    const int stop = chunk_end(it);
+    if (!wave_any(active && vc0 != 1))
+      vthree_s3_chunk<1>(s0, s1, s2, s3, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+    else
+      vthree_s3_chunk<0>(s0, s1, s2, s3, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+  }
+  if (entered) {
+    if (dA0) set_vel_a(B, a0, V2(vA0), wA0);
+    set_vel_b(B, x, V2(vX), wX);
+    if (s3) set_vel_b(B, y, V2(vY), wY);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    s1.ni[j] = s3 ? s1.ni[j] : ni1[j];
+    s1.ti[j] = s3 ? s1.ti[j] : ti1[j];
+    s2.ni[j] = s3 ? s2.ni[j] : ni2[j];
+    s2.ti[j] = s3 ? s2.ti[j] : ti2[j];
+  }
+}
+
 // General family: the slot loop over the body file (any island size, register or HBM slots).  Islands
 // share no dynamic body, so each island's state (its bodies' velocities, its contacts' impulses) evolves
 // on its own: an island whose state is periodic retires on its own (its slots leave `live` and are no
@@ -922,7 +1018,26 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3], Ph
     while (wave_any(active)) {
       const int nl = __popc(live);
       HK_FAM_T0();
-      if (wave_any(active && nl > 2)) {
+      // S3 family (vthree_s3_family): every running lane is an S3 lane (its three live contacts in slots 0-2) or a
+      // one-contact rider
+      bool s3 = false, s3ok = false;
+      if constexpr (SlotCap<SL>::value >= 3) {
+        s3 = active && nl == 3 && live == 7u && s3_shape(S.s[0], S.s[1], S.s[2]);
+        s3ok = !wave_any(active && !s3 && nl != 1);
+      }
+      if (wave_any(active && nl > 2) && s3ok) {
+        if constexpr (SlotCap<SL>::value >= 3) {
+          const int j0 = nl == 1 ? __ffs(live) - 1 : 0;
+          const bool perm = wave_any(active && j0 != 0);
+          if (perm) slot_swap(S, 0, j0);
+          const bool entered = active;
+          if (s3) HK_HOST_DIAG_INC(2);
+          vthree_s3_family(S.s[0], S.s[1], S.s[2], B, s3, it, active, first);
+          live = entered && !active ? 0u : live;
+          if (perm) slot_swap(S, 0, j0);
+          HK_FAM_ADD(T, 0);
+        }
+      } else if (wave_any(active && nl > 2)) {
         vgen_family(S, B, nc, live, isl_of, it, active, first, true);
         HK_FAM_ADD(T, 0);
       } else {

@@ -43,7 +43,8 @@ def lib():
 
 def velocity_diag():
     """Velocity-loop coverage counters of the host build since the last call (and clears them): [0] islands
-    retired while another island of the lane kept iterating, [1] live contacts swapped into slots 0/1."""
+    retired while another island of the lane kept iterating, [1] live contacts swapped into slots 0/1, [2] S3 lanes
+    entering the three-contact shape family, [3] S2 two-contact shape chunks (hk_solver.h)."""
     out = np.zeros(4, np.uint64)
     lib().hkh_diag(out.ctypes.data)
     return out

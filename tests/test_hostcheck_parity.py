@@ -198,3 +198,16 @@ def test_step_record_matches_outputs_and_state(oracle):
         held += int((aux[:, 0] > 0).sum())
     assert aux[:, 3].sum() > 0 and held > 0  # goals and holds happened
 
+
+
+def test_shape_families_vs_oracle(oracle):
+    """The tail's shape-specialised velocity loops (r06, hk_solver.h): the S2 two-contact chunk (contact 1's body B
+    aliased to contact 0's body A, contact 1 static-A) and the S3 three-contact family (wall-puck, player-puck,
+    wall-player with the two dynamic bodies in locals) both run in a bit-exact lockstep of the strong-vs-strong
+    bench workload against the oracle.  (The host build runs one lane at a time, so the one-contact riders of those
+    loops run on the GPU only: tests/test_gpu_parity.py.)"""
+    velocity_diag()
+    out = _vec_lockstep(oracle, 1024, 400, 0, ("strong", "strong"), seed=41)
+    assert "field" not in out, out
+    d = velocity_diag()
+    assert d[2] > 0 and d[3] > 0, d
