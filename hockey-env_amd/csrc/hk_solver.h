@@ -745,6 +745,81 @@ HK_DEV void vtwo_s2_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s2, 
   for (int k = 0; k < 20; ++k) t.sn[k] = sn[k];
 }
 
+// The aliased two-contact chunk for mixed waves (r06): every running lane is an S2 lane (b1 == a0, contact 1 static
+// A), a "TB" lane (b1 == b0: contact 1's body B is contact 0's body B, e.g. wall-puck then player-puck, or a TOI
+// mini-island's two static contacts on one body), or a one-contact rider -- with any point counts (scripts/
+// tail_shape_study.c: the slowest waves mostly mix S2 lanes whose contact 1 has one and two points, or run TB
+// lanes).  The shared body has one home per lane (contact 0's A for S2, its B for TB): contact 1 reads it through one
+// select per component and commits its update with one per component and shape, instead of the generic chunk's
+// refresh selects after both contacts and its exec-mask guard; contact 1's own body A lives in locals (static for
+// S2, +0 by its lane mask).  Riders as in vtwo_s2_chunk.  Bit-identical to the generic chunk for every lane.
+template <int kP0, int kP1>
+HK_DEV void vtwo_alias_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s2, bool tb, bool dA0, bool dA1,
+                             uint32_t mA0, uint32_t mA1, int &it, int stop, int first, bool &active, bool &on0,
+                             bool &on1) {
+  f2 vA0 = t.vA0, vB0 = t.vB0, vA1 = t.vA1;
+  float wA0 = t.wA0, wB0 = t.wB0, wA1 = t.wA1;
+  uint32_t sn[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) sn[k] = t.sn[k];
+  if (active && two) HK_HOST_DIAG_INC(3);
+  const float ni0 = s1.ni[0], ni1 = s1.ni[1], ti0 = s1.ti[0], ti1 = s1.ti[1];
+  HK_MARK(vtwo_alias_begin);
+  for (; it < stop && active; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vA0 = f2{mask_f(vA0[0], mA0), mask_f(vA0[1], mA0)};
+      wA0 = mask_f(wA0, mA0);
+      fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
+      f2 vB1 = sel2(s2, vA0, vB0);  // the shared body (a rider: a dummy copy)
+      float wB1 = s2 ? wA0 : wB0;
+      vA1 = f2{mask_f(vA1[0], mA1), mask_f(vA1[1], mA1)};
+      wA1 = mask_f(wA1, mA1);
+      fslot_solve_velocity_p<false, kP1>(s1, vA1, wA1, vB1, wB1);
+      vA0 = sel2(s2, vB1, vA0);
+      wA0 = s2 ? wB1 : wA0;
+      vB0 = sel2(tb, vB1, vB0);
+      wB0 = tb ? wB1 : wB0;
+    }
+    const f2 sh = sel2(s2, vA0, vB0);
+    const float wsh = s2 ? wA0 : wB0;
+    const uint32_t x[20] = {__float_as_uint(vB0[0]), __float_as_uint(vB0[1]), __float_as_uint(wB0),
+                            dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
+                            dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
+                            __float_as_uint(s0.ti[0]), __float_as_uint(s0.ti[1]),
+                            two ? __float_as_uint(sh[0]) : 0u, two ? __float_as_uint(sh[1]) : 0u,
+                            two ? __float_as_uint(wsh) : 0u, dA1 ? __float_as_uint(vA1[0]) : 0u,
+                            dA1 ? __float_as_uint(vA1[1]) : 0u, dA1 ? __float_as_uint(wA1) : 0u,
+                            two ? __float_as_uint(s1.ni[0]) : 0u, two ? __float_as_uint(s1.ni[1]) : 0u,
+                            two ? __float_as_uint(s1.ti[0]) : 0u, two ? __float_as_uint(s1.ti[1]) : 0u};
+    uint32_t d = 0u;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+      d |= x[k] ^ sn[k];
+      sn[k] = x[k];
+    }
+    if (it + 3 >= first && d == 0u) {  // no lane here is split over two islands (see the dispatch)
+      on0 = false;
+      on1 = false;
+      active = false;
+    }
+  }
+  HK_MARK(vtwo_alias_end);
+  if (it >= kVelIters) active = false;
+  const bool shaped = s2 || tb;  // only these lanes' contact-1 copies changed (others ran no iteration here or are riders)
+  t.vA0 = vA0; t.vB0 = vB0; t.wA0 = wA0; t.wB0 = wB0;
+  t.vB1 = sel2(shaped, sel2(s2, vA0, vB0), t.vB1);
+  t.wB1 = shaped ? (s2 ? wA0 : wB0) : t.wB1;
+  t.vA1 = sel2(tb, vA1, t.vA1);
+  t.wA1 = tb ? wA1 : t.wA1;
+  s1.ni[0] = two ? s1.ni[0] : ni0;
+  s1.ni[1] = two ? s1.ni[1] : ni1;
+  s1.ti[0] = two ? s1.ti[0] : ti0;
+  s1.ti[1] = two ? s1.ti[1] : ti1;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) t.sn[k] = sn[k];
+}
+
 // runs until every lane is done or no running lane has both contacts live (then the one-contact family takes
 // over).  on0 / on1 in: the lane's contacts that iterate (on1 == two); out: the ones still unfinished.
 HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &active, int first, bool &on0,
@@ -771,6 +846,7 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
   for (int k = 0; k < 20; ++k) t.sn[k] = 0u;
   // the S2 shape (see vtwo_s2_chunk): one island, contact 1's body A static and its body B contact 0's body A
   const bool s2 = two && !sep && !dA1 && b1a0;
+  const bool tb = two && !sep && b1b0;  // TB lanes (see vtwo_alias_chunk)
   while (wave_any(active) && wave_any(active && on0 && on1)) {
     const int stop = chunk_end(it);
     // S2 chunk: every running lane is an S2 lane with both contacts live, or a one-contact rider (two == false)
@@ -785,6 +861,17 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
         vtwo_s2_chunk<1, 2>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
       else
         vtwo_s2_chunk<0, 2>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
+    } else if (!wave_any(active && (!on0 || (two && !((s2 || tb) && on1))))) {
+      // aliased chunk: S2 and TB lanes with both contacts live, and one-contact riders
+      const bool p0 = !wave_any(active && vc0 != 1), p1 = !wave_any(active && two && vc1 != 1);
+      if (p0 && p1)
+        vtwo_alias_chunk<1, 1>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+      else if (p0)
+        vtwo_alias_chunk<1, 0>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+      else if (p1)
+        vtwo_alias_chunk<0, 1>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+      else
+        vtwo_alias_chunk<0, 0>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
     } else if (wave_any(active && !on0))
       vtwo_chunk<0, 0, true>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                              on1);

@@ -35,6 +35,7 @@ static __thread uint32_t g_x[VEL_ITERS][MAXW];
 static __thread int64_t g_arena = -1;
 static arena_rec *g_rec;
 static int g_on;
+static int64_t toi_n[10000], toi_it[10000], toi_long[10000];
 
 static void ts_arena(int64_t i) { g_arena = i; }
 
@@ -53,10 +54,18 @@ static void ts_hook(const void *Sv, const void *Vlv, int nb, int it, int toi) {
       memcpy(&x[n++], &S->vc[i].p[j].ni, 4);
       memcpy(&x[n++], &S->vc[i].p[j].ti, 4);
     }
-  if (it != VEL_ITERS - 1 || !g_on || toi || g_arena < 0) return;
+  if (it != VEL_ITERS - 1 || !g_on || g_arena < 0) return;
   int cur = VEL_ITERS;
   for (int k = 7; k < VEL_ITERS; k += 4)
     if (!memcmp(g_x[k], g_x[k - 4], 4 * n)) { cur = k + 1; break; }
+  if (toi) { /* TOI mini-island solves: contacts x (static A?, points) and iterations run */
+    int key = S->n > 3 ? 3 : S->n;
+    for (int i = 0; i < S->n && i < 3; ++i) key = key * 10 + S->vc[i].count + (S->vc[i].mA != 0.0f ? 2 : 0);
+    __atomic_fetch_add(&toi_n[key % 10000], 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&toi_it[key % 10000], cur, __ATOMIC_RELAXED);
+    if (cur >= 100) __atomic_fetch_add(&toi_long[key % 10000], 1, __ATOMIC_RELAXED);
+    return;
+  }
   arena_rec *r = &g_rec[g_arena];
   if (r->ns >= MAXSOLVE) return;
   solve_rec *s = &r->s[r->ns++];
@@ -105,6 +114,7 @@ static char keys[NKEY][64];
 static double key_w[3][NKEY];
 static int nkeys;
 static double gen_mix[2][2];
+static double slow_tot, slow_fam[5];
 static int key_id(const char *k) {
   for (int i = 0; i < nkeys; ++i)
     if (!strcmp(keys[i], k)) return i;
@@ -130,8 +140,12 @@ int main(int argc, char **argv) {
     g_on = 1;
     hkov_step(v, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     g_on = 0;
+    double best = -1, best_fam[5] = {0, 0, 0, 0, 0};
+    char best_sig[256] = "";
     for (int w0 = 0; w0 + 64 <= n; w0 += 64) {
       ++waves;
+      double wf[5] = {0, 0, 0, 0, 0};
+      char wsig[256] = "";
       /* the wave's last chunk with a running lane: the chunk that ends the wave's velocity phase */
       int last_c = -1;
       for (int c = 0; c < 8; ++c)
@@ -156,6 +170,34 @@ int main(int argc, char **argv) {
         if (!maxlive) continue;
         const int fam = maxlive > 2 ? 2 : maxlive - 1;
         fam_it[fam] += len;
+        {
+          /* cost-model family: S2 / S3 when every running multi-contact lane has that shape (riders allowed) */
+          const char *k = multi_key >= 0 ? keys[multi_key] : "";
+          int cf;
+          double cost;
+          if (fam == 0) { cf = 0; cost = 86; }
+          else if (fam == 1) {
+            const int s2 = uniform && (!strcmp(k, "[01p1][s0p1]") || !strcmp(k, "[01p1][s0p2]"));
+            cf = s2 ? 2 : 1; cost = s2 ? 140 : 225;
+          } else {
+            const int s3 = uniform && !strcmp(k, "[s0p1][10p1][s1p1]") && nmulti > 0;
+            cf = s3 ? 3 : 4; cost = s3 ? 190 : 109.0 * maxlive;
+          }
+          wf[cf] += cost * len;
+          if (cf == 1 && c >= 3) { /* generic two-contact chunk: the distinct multi-contact shapes running */
+            char set[256] = "";
+            for (int l = 0; l < 64; ++l) {
+              char key[64];
+              int live;
+              shape_key(&g_rec[w0 + l], t, key, &live);
+              if (live >= 2 && !strstr(set, key) && strlen(set) + strlen(key) + 2 < sizeof set) {
+                strcat(set, key);
+                strcat(set, " ");
+              }
+            }
+            if (!wsig[0]) strncpy(wsig, set, sizeof wsig - 1);
+          }
+        }
         /* uniform: every running multi-contact lane has the same shape and no one-contact lane rides along */
         const int uni = fam == 0 || (uniform && !anyone);
         if (uni) uni_it[fam] += len;
@@ -166,6 +208,10 @@ int main(int argc, char **argv) {
         }
         if (fam > 0 && uniform && multi_key >= 0 && c >= 4) key_w[anyone ? 1 : 0][multi_key] += len;
         if (c == last_c && fam > 0 && multi_key >= 0) key_w[2][multi_key] += 1;
+        if (c == 7) {
+          const double tot = wf[0] + wf[1] + wf[2] + wf[3] + wf[4];
+          if (tot > best) { best = tot; memcpy(best_fam, wf, sizeof wf); strcpy(best_sig, wsig); }
+        }
         if (fam == 2 && c >= 4) { /* general-family tail chunks: the live-contact counts of the running lanes */
           int cnt[5] = {0, 0, 0, 0, 0};
           for (int l = 0; l < 64; ++l) {
@@ -178,8 +224,16 @@ int main(int argc, char **argv) {
         }
       }
     }
+    slow_tot += best;
+    printf("step %d slowest wave %.0f slots (one %.0f two-generic %.0f S2 %.0f S3 %.0f general %.0f): generic-two shapes %s\n",
+           st, best, best_fam[0], best_fam[1], best_fam[2], best_fam[3], best_fam[4], best_sig);
+    for (int f = 0; f < 5; ++f) slow_fam[f] += best_fam[f];
   }
   printf("%d arenas x %d steps after %d (%lld waves)\n", n, steps, pre, (long long)waves);
+  printf("cost model (issue slots per iteration: one 86, two generic 225, two S2 140, S3 190, general 109 per live "
+         "contact of the widest lane): slowest wave per step, mean over steps %.0f slots; its split one / two-generic "
+         "/ two-S2 / S3 / general: %.0f %.0f %.0f %.0f %.0f\n", slow_tot / steps, slow_fam[0] / steps,
+         slow_fam[1] / steps, slow_fam[2] / steps, slow_fam[3] / steps, slow_fam[4] / steps);
   const char *fn[3] = {"one", "two", "general"};
   for (int f = 0; f < 3; ++f)
     printf("family %-8s iterations per wave %.2f; all running multi-contact lanes one shape, no rider: %.1f%%; "
@@ -190,12 +244,18 @@ int main(int argc, char **argv) {
   printf("shapes of uniform tail chunks (it >= 56), iterations per 1000 waves: [no riders] [with one-contact riders]"
          " | waves whose last chunk has this shape among its multi-contact lanes\n");
   for (int i = 0; i < nkeys; ++i)
-    if (key_w[0][i] + key_w[1][i] >= 0.002 * waves || key_w[2][i] >= 0.001 * waves)
+    if (key_w[0][i] + key_w[1][i] >= 0.002 * waves || key_w[2][i] >= 0.001 * waves ||
+        (strlen(keys[i]) >= 24 && key_w[2][i] >= 1))
       printf("  %-40s %9.1f %9.1f | %7.0f\n", keys[i], 1000 * key_w[0][i] / waves, 1000 * key_w[1][i] / waves,
              key_w[2][i]);
   printf("general-family tail iterations per 1000 waves by rider kinds: alone %.1f, +1-contact %.1f, +2-contact "
          "%.1f, +both %.1f\n", 1000 * gen_mix[0][0] / waves, 1000 * gen_mix[1][0] / waves, 1000 * gen_mix[0][1] / waves,
          1000 * gen_mix[1][1] / waves);
+  printf("TOI solves by shape (contacts, then per contact points + 2 if body A dynamic): count, mean iterations, "
+         ">= 100 iterations\n");
+  for (int k = 0; k < 10000; ++k)
+    if (toi_n[k]) printf("  %5d %8lld %7.1f %8lld\n", k, (long long)toi_n[k], (double)toi_it[k] / toi_n[k],
+                         (long long)toi_long[k]);
   hkov_destroy(v);
   return 0;
 }
