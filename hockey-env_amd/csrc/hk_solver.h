@@ -905,18 +905,21 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
 
 // The tail's three-contact shape (r06, scripts/tail_shape_study.c): one island of three one-point contacts, slot 0
 // = (static, X), slot 1 = (Y, X), slot 2 = (static, Y) -- wall-puck, player-puck, wall-player -- optionally with
-// one-contact lanes riding along (their contact swapped into slot 0).  X and Y live in locals, aliased at compile
-// time, instead of the general family's body-file gathers and scatters (~30 selects per contact): slot 0 runs the
-// generic row on (A0, X) (a rider's own bodies; an S3 lane's A0 is static, +0), slot 1 the dynamic row on (Y, X),
-// whose update of X a rider discards (one select per component; its Y is a dummy never written back), slot 2 the
-// static-body-A row on Y.  Riders' slot 1 / 2 impulses are restored at the end (another island's retired contacts
-// may sit there).  The snapshot covers X, Y, A0 and the three contacts' impulses (a rider: its own body pair and
-// impulses), the island's whole state, so the periodic exit stays exact; this family starts its own chain.  Each S3
-// lane's float operations are the general family's, in its order.  Runs while some S3 lane iterates.
-template <int kP0>
-HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, uint32_t mA0, bool dA0, f2 &vA0, float &wA0,
-                            f2 &vX, float &wX, f2 &vY, float &wY, uint32_t (&sn)[17], int &it, int stop, int first,
-                            bool &active) {
+// riders: one-contact lanes (their contact swapped into slot 0) and S2 two-contact lanes (player-puck, wall-player:
+// contact 0 in slot 0, contact 1 in slot 2; the slowest waves of the bench workload mostly hold S3 and S2 lanes
+// together).  X and Y live in locals, aliased at compile time, instead of the general family's body-file gathers
+// and scatters (~30 selects per contact): slot 0 runs the generic row on (A0, X) (a rider's own bodies; an S3 lane's
+// A0 is static, +0), slot 1 the dynamic row on (Y, X), whose update of X a non-S3 lane discards (one select per
+// component), slot 2 the static-body-A row on Y, which an S2 lane points at its body A0 (its contact 1's body B)
+// with one select per component before and after.  Non-S3 lanes' slot 1 impulses, and one-contact riders' slot 2
+// impulses, are restored at the end (another island's retired contacts may sit there).  The snapshot covers X, Y,
+// A0 and the three slots' impulses that the lane solves: the island's whole state, so the periodic exit stays exact;
+// this family starts its own chain.  Each lane's float operations are the general family's, in its order.  Runs
+// while some S3 lane iterates.
+template <int kP0, int kP2>
+HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, bool s2l, uint32_t mA0, bool dA0, f2 &vA0,
+                            float &wA0, f2 &vX, float &wX, f2 &vY, float &wY, uint32_t (&sn)[19], int &it, int stop,
+                            int first, bool &active) {
   HK_MARK(vthree_begin);
   for (; it < stop && active; it += 4) {
 #pragma unroll
@@ -929,21 +932,27 @@ HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, uint32_t m
       fslot_solve_velocity_p<false, 1>(s1, vY, wY, vB1, wB1);
       vX = sel2(s3, vB1, vX);
       wX = s3 ? wB1 : wX;
+      vY = sel2(s2l, vA0, vY);  // an S2 lane's contact 1 acts on its body A0
+      wY = s2l ? wA0 : wY;
       f2 vA2 = f2{0.0f, 0.0f};
       float wA2 = 0.0f;
-      fslot_solve_velocity_p<true, 1>(s2, vA2, wA2, vY, wY);
+      fslot_solve_velocity_p<true, kP2>(s2, vA2, wA2, vY, wY);
+      vA0 = sel2(s2l, vY, vA0);
+      wA0 = s2l ? wY : wA0;
     }
-    const uint32_t x[17] = {__float_as_uint(vX[0]), __float_as_uint(vX[1]), __float_as_uint(wX),
+    const bool sl2 = s3 || s2l;  // lanes that solve slot 2
+    const uint32_t x[19] = {__float_as_uint(vX[0]), __float_as_uint(vX[1]), __float_as_uint(wX),
                             dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
                             dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
                             __float_as_uint(s0.ti[0]), __float_as_uint(s0.ti[1]),
                             s3 ? __float_as_uint(vY[0]) : 0u, s3 ? __float_as_uint(vY[1]) : 0u,
                             s3 ? __float_as_uint(wY) : 0u, s3 ? __float_as_uint(s1.ni[0]) : 0u,
-                            s3 ? __float_as_uint(s1.ti[0]) : 0u, s3 ? __float_as_uint(s2.ni[0]) : 0u,
-                            s3 ? __float_as_uint(s2.ti[0]) : 0u};
+                            s3 ? __float_as_uint(s1.ti[0]) : 0u, sl2 ? __float_as_uint(s2.ni[0]) : 0u,
+                            sl2 ? __float_as_uint(s2.ti[0]) : 0u, sl2 ? __float_as_uint(s2.ni[1]) : 0u,
+                            sl2 ? __float_as_uint(s2.ti[1]) : 0u};
     uint32_t d = 0u;
 #pragma unroll
-    for (int k = 0; k < 17; ++k) {
+    for (int k = 0; k < 19; ++k) {
       d |= x[k] ^ sn[k];
       sn[k] = x[k];
     }
@@ -956,13 +965,19 @@ HK_DEV bool s3_shape(const FSlot &s0, const FSlot &s1, const FSlot &s2) {
   return fs_bA(s0) >= 3 && fs_bA(s2) >= 3 && fs_bA(s1) < 3 && fs_bB(s0) == fs_bB(s1) && fs_bA(s1) == fs_bB(s2) &&
          fs_vcount(s0) == 1 && fs_vcount(s1) == 1 && fs_vcount(s2) == 1;
 }
-// s3: this lane is an S3 lane (else a one-contact rider with its contact in slot 0)
-HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, int &it, bool &active, int first) {
+// S2 pair from slot bits: contact 1 (bits1) static A, its body B contact 0's body A, one island
+HK_DEV bool s2_bits(int bits0, int bits1) {
+  const int a0 = (bits0 >> 7) & 15, a1 = (bits1 >> 7) & 15, b1 = (bits1 >> 11) & 15;
+  return a1 >= 3 && b1 == a0 && ((bits0 >> 5) & 3) == ((bits1 >> 5) & 3);
+}
+// s3: an S3 lane; s2l: an S2 lane (contact 0 in slot 0, contact 1 in slot 2); else a one-contact rider (slot 0)
+HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, bool s2l, int &it, bool &active,
+                             int first) {
   const bool entered = active;
   const int a0 = fs_bA(s0), x = fs_bB(s0), y = s3 ? fs_bA(s1) : x;
   const bool dA0 = a0 < 3;
   const uint32_t mA0 = lane_mask(dA0);
-  const int vc0 = fs_vcount(s0);
+  const int vc0 = fs_vcount(s0), vc2 = s2l ? fs_vcount(s2) : 1;
   v2 q;
   float wA0, wX, wY;
   get_vel_a(B, a0, q, wA0);
@@ -973,27 +988,31 @@ HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, i
   f2 vY = F2(q);
   const float ni1[2] = {s1.ni[0], s1.ni[1]}, ti1[2] = {s1.ti[0], s1.ti[1]};
   const float ni2[2] = {s2.ni[0], s2.ni[1]}, ti2[2] = {s2.ti[0], s2.ti[1]};
-  uint32_t sn[17];
+  uint32_t sn[19];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) sn[k] = 0u;
+  for (int k = 0; k < 19; ++k) sn[k] = 0u;
   while (wave_any(active && s3)) {
     const int stop = chunk_end(it);
-    if (!wave_any(active && vc0 != 1))
-      vthree_s3_chunk<1>(s0, s1, s2, s3, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+    const bool p0 = !wave_any(active && vc0 != 1), p2 = !wave_any(active && vc2 != 1);
+    if (p0 && p2)
+      vthree_s3_chunk<1, 1>(s0, s1, s2, s3, s2l, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+    else if (p2)
+      vthree_s3_chunk<0, 1>(s0, s1, s2, s3, s2l, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
     else
-      vthree_s3_chunk<0>(s0, s1, s2, s3, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+      vthree_s3_chunk<0, 0>(s0, s1, s2, s3, s2l, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
   }
   if (entered) {
     if (dA0) set_vel_a(B, a0, V2(vA0), wA0);
     set_vel_b(B, x, V2(vX), wX);
     if (s3) set_vel_b(B, y, V2(vY), wY);
   }
+  const bool sl2 = s3 || s2l;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     s1.ni[j] = s3 ? s1.ni[j] : ni1[j];
     s1.ti[j] = s3 ? s1.ti[j] : ti1[j];
-    s2.ni[j] = s3 ? s2.ni[j] : ni2[j];
-    s2.ti[j] = s3 ? s2.ti[j] : ti2[j];
+    s2.ni[j] = sl2 ? s2.ni[j] : ni2[j];
+    s2.ti[j] = sl2 ? s2.ti[j] : ti2[j];
   }
 }
 
@@ -1105,23 +1124,44 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3], Ph
     while (wave_any(active)) {
       const int nl = __popc(live);
       HK_FAM_T0();
-      // S3 family (vthree_s3_family): every running lane is an S3 lane (its three live contacts in slots 0-2) or a
-      // one-contact rider
-      bool s3 = false, s3ok = false;
+      // S3 family (vthree_s3_family): every running lane is an S3 lane (its three live contacts in slots 0-2), an
+      // S2 lane (two live contacts) or a one-contact rider
+      bool s3 = false, s2l = false, s3ok = false;
+      int j0 = 0, j1 = 1;
       if constexpr (SlotCap<SL>::value >= 3) {
         s3 = active && nl == 3 && live == 7u && s3_shape(S.s[0], S.s[1], S.s[2]);
-        s3ok = !wave_any(active && !s3 && nl != 1);
+        j0 = nl >= 1 ? __ffs(live) - 1 : 0;
+        j1 = nl >= 2 ? __ffs(live & (live - 1u)) - 1 : 1;
+        if (wave_any(s3)) {
+          int b0 = 0, b1 = 0;  // the live slots' bits, by select (slot indices are runtime per lane)
+#pragma unroll
+          for (int q = 0; q < SlotCap<SL>::value; ++q) {
+            b0 = q == j0 ? S.s[q].bits : b0;
+            b1 = q == j1 ? S.s[q].bits : b1;
+          }
+          s2l = active && nl == 2 && s2_bits(b0, b1);
+        }
+        s3ok = wave_any(s3) && !wave_any(active && !s3 && !s2l && nl != 1);
       }
-      if (wave_any(active && nl > 2) && s3ok) {
+      if (s3ok) {
         if constexpr (SlotCap<SL>::value >= 3) {
-          const int j0 = nl == 1 ? __ffs(live) - 1 : 0;
-          const bool perm = wave_any(active && j0 != 0);
-          if (perm) slot_swap(S, 0, j0);
+          // riders' and S2 lanes' contact 0 to slot 0; an S2 lane's contact 1 to slot 2 (j0 < j1, so the first swap
+          // leaves j1 in place)
+          const bool mv0 = !s3 && j0 != 0, mv12 = s2l && j1 == 1;
+          const bool mv23 = SlotCap<SL>::value >= 4 && s2l && j1 == 3;
+          const bool any0 = wave_any(active && mv0), any12 = wave_any(mv12), any23 = wave_any(mv23);
+          if (any0) slot_swap(S, 0, mv0 ? j0 : 0);
+          if (any12) slot_swap(S, 1, mv12 ? 2 : 1);
+          if constexpr (SlotCap<SL>::value >= 4)
+            if (any23) slot_swap(S, 2, mv23 ? 3 : 2);
           const bool entered = active;
           if (s3) HK_HOST_DIAG_INC(2);
-          vthree_s3_family(S.s[0], S.s[1], S.s[2], B, s3, it, active, first);
+          vthree_s3_family(S.s[0], S.s[1], S.s[2], B, s3, s2l, it, active, first);
           live = entered && !active ? 0u : live;
-          if (perm) slot_swap(S, 0, j0);
+          if constexpr (SlotCap<SL>::value >= 4)
+            if (any23) slot_swap(S, 2, mv23 ? 3 : 2);
+          if (any12) slot_swap(S, 1, mv12 ? 2 : 1);
+          if (any0) slot_swap(S, 0, mv0 ? j0 : 0);
           HK_FAM_ADD(T, 0);
         }
       } else if (wave_any(active && nl > 2)) {

@@ -177,14 +177,27 @@ int main(int argc, char **argv) {
           double cost;
           if (fam == 0) { cf = 0; cost = 86; }
           else if (fam == 1) {
-            const int s2 = uniform && (!strcmp(k, "[01p1][s0p1]") || !strcmp(k, "[01p1][s0p2]"));
-            cf = s2 ? 2 : 1; cost = s2 ? 140 : 225;
+            /* S2 / aliased: every multi-contact lane is S2 ([01p*][s0p*]) or TB ([*0p*][*0p*]: contact 1's B is
+             * contact 0's B) */
+            int all_alias = 1, all_s2 = 1;
+            for (int l = 0; l < 64; ++l) {
+              char key[64];
+              int live;
+              shape_key(&g_rec[w0 + l], t, key, &live);
+              if (live != 2) continue;
+              const int is_s2 = !strncmp(key, "[01p", 4) && !strncmp(key + 6, "[s0p", 4);
+              const int is_tb = key[2] == '0' && key[8] == '0' && key[7] != 's' ? 1 : (key[2] == '0' && key[8] == '0');
+              if (!is_s2) all_s2 = 0;
+              if (!is_s2 && !is_tb) all_alias = 0;
+            }
+            cf = all_s2 ? 2 : all_alias ? 2 : 1;
+            cost = all_s2 && uniform ? 140 : all_alias ? 180 : 225;
           } else {
             const int s3 = uniform && !strcmp(k, "[s0p1][10p1][s1p1]") && nmulti > 0;
             cf = s3 ? 3 : 4; cost = s3 ? 190 : 109.0 * maxlive;
           }
           wf[cf] += cost * len;
-          if (cf == 1 && c >= 3) { /* generic two-contact chunk: the distinct multi-contact shapes running */
+          if ((cf == 1 || cf == 4) && c >= 3) { /* generic two-contact or general chunk: the distinct multi-contact shapes running */
             char set[256] = "";
             for (int l = 0; l < 64; ++l) {
               char key[64];
