@@ -753,16 +753,12 @@ HK_DEV void vtwo_s2_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s2, 
 // select per component and commits its update with one per component and shape, instead of the generic chunk's
 // refresh selects after both contacts and its exec-mask guard; contact 1's own body A lives in locals (static for
 // S2, +0 by its lane mask).  Riders as in vtwo_s2_chunk.  Bit-identical to the generic chunk for every lane.
-// kSep: some running lane is a SEP lane (two islands, no shared dynamic body; contact 1 on its own body pair, both
-// contacts still iterating).  Its islands then retire together, when both are periodic: an island that became
-// periodic earlier keeps iterating inside its period, so at that common exit (a snapshot boundary, 3 mod 4) its
-// state is still the 180-iteration one -- the same bits as retiring it on its own.
-template <int kP0, int kP1, bool kSep>
+template <int kP0, int kP1>
 HK_DEV void vtwo_alias_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s2, bool tb, bool dA0, bool dA1,
                              uint32_t mA0, uint32_t mA1, int &it, int stop, int first, bool &active, bool &on0,
                              bool &on1) {
-  f2 vA0 = t.vA0, vB0 = t.vB0, vA1 = t.vA1, vB1o = t.vB1;  // vB1o: a SEP lane's own contact-1 body B
-  float wA0 = t.wA0, wB0 = t.wB0, wA1 = t.wA1, wB1o = t.wB1;
+  f2 vA0 = t.vA0, vB0 = t.vB0, vA1 = t.vA1;
+  float wA0 = t.wA0, wB0 = t.wB0, wA1 = t.wA1;
   uint32_t sn[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) sn[k] = t.sn[k];
@@ -777,10 +773,6 @@ HK_DEV void vtwo_alias_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s
       fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vB0, wB0);
       f2 vB1 = sel2(s2, vA0, vB0);  // the shared body (a rider: a dummy copy)
       float wB1 = s2 ? wA0 : wB0;
-      if constexpr (kSep) {
-        vB1 = sel2(s2 || tb, vB1, vB1o);
-        wB1 = (s2 || tb) ? wB1 : wB1o;
-      }
       vA1 = f2{mask_f(vA1[0], mA1), mask_f(vA1[1], mA1)};
       wA1 = mask_f(wA1, mA1);
       fslot_solve_velocity_p<false, kP1>(s1, vA1, wA1, vB1, wB1);
@@ -788,17 +780,9 @@ HK_DEV void vtwo_alias_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s
       wA0 = s2 ? wB1 : wA0;
       vB0 = sel2(tb, vB1, vB0);
       wB0 = tb ? wB1 : wB0;
-      if constexpr (kSep) {
-        vB1o = vB1;
-        wB1o = wB1;
-      }
     }
-    f2 sh = sel2(s2, vA0, vB0);
-    float wsh = s2 ? wA0 : wB0;
-    if constexpr (kSep) {
-      sh = sel2(s2 || tb, sh, vB1o);
-      wsh = (s2 || tb) ? wsh : wB1o;
-    }
+    const f2 sh = sel2(s2, vA0, vB0);
+    const float wsh = s2 ? wA0 : wB0;
     const uint32_t x[20] = {__float_as_uint(vB0[0]), __float_as_uint(vB0[1]), __float_as_uint(wB0),
                             dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
                             dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
@@ -823,12 +807,11 @@ HK_DEV void vtwo_alias_chunk(FSlot &s0, FSlot &s1, TwoState &t, bool two, bool s
   HK_MARK(vtwo_alias_end);
   if (it >= kVelIters) active = false;
   const bool shaped = s2 || tb;  // only these lanes' contact-1 copies changed (others ran no iteration here or are riders)
-  const bool sepl = kSep && two && !shaped;  // SEP lanes (riders have two == false)
   t.vA0 = vA0; t.vB0 = vB0; t.wA0 = wA0; t.wB0 = wB0;
-  t.vB1 = sel2(shaped, sel2(s2, vA0, vB0), sel2(sepl, vB1o, t.vB1));
-  t.wB1 = shaped ? (s2 ? wA0 : wB0) : (sepl ? wB1o : t.wB1);
-  t.vA1 = sel2(tb || sepl, vA1, t.vA1);
-  t.wA1 = (tb || sepl) ? wA1 : t.wA1;
+  t.vB1 = sel2(shaped, sel2(s2, vA0, vB0), t.vB1);
+  t.wB1 = shaped ? (s2 ? wA0 : wB0) : t.wB1;
+  t.vA1 = sel2(tb, vA1, t.vA1);
+  t.wA1 = tb ? wA1 : t.wA1;
   s1.ni[0] = two ? s1.ni[0] : ni0;
   s1.ni[1] = two ? s1.ni[1] : ni1;
   s1.ti[0] = two ? s1.ti[0] : ti0;
@@ -864,8 +847,6 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
   // the S2 shape (see vtwo_s2_chunk): one island, contact 1's body A static and its body B contact 0's body A
   const bool s2 = two && !sep && !dA1 && b1a0;
   const bool tb = two && !sep && b1b0;  // TB lanes (see vtwo_alias_chunk)
-  // SEP lanes: two islands with no shared dynamic body (a static body A both contacts touch is +0 in both)
-  const bool sepx = two && sep && !(dA0 && (a1a0 || b1a0)) && !(b1b0 || a1b0);
   while (wave_any(active) && wave_any(active && on0 && on1)) {
     const int stop = chunk_end(it);
     // S2 chunk: every running lane is an S2 lane with both contacts live, or a one-contact rider (two == false)
@@ -880,19 +861,17 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
         vtwo_s2_chunk<1, 2>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
       else
         vtwo_s2_chunk<0, 2>(s0, s1, t, two, s2, dA0, mA0, it, stop, first, active, on0, on1);
-    } else if (!wave_any(active && (!on0 || (two && !((s2 || tb || sepx) && on1))))) {
-      // aliased chunk: S2, TB and SEP lanes with both contacts live, and one-contact riders
+    } else if (!wave_any(active && (!on0 || (two && !((s2 || tb) && on1))))) {
+      // aliased chunk: S2 and TB lanes with both contacts live, and one-contact riders
       const bool p0 = !wave_any(active && vc0 != 1), p1 = !wave_any(active && two && vc1 != 1);
-      if (wave_any(active && two && sepx))
-        vtwo_alias_chunk<0, 0, true>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
-      else if (p0 && p1)
-        vtwo_alias_chunk<1, 1, false>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+      if (p0 && p1)
+        vtwo_alias_chunk<1, 1>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
       else if (p0)
-        vtwo_alias_chunk<1, 0, false>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+        vtwo_alias_chunk<1, 0>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
       else if (p1)
-        vtwo_alias_chunk<0, 1, false>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+        vtwo_alias_chunk<0, 1>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
       else
-        vtwo_alias_chunk<0, 0, false>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
+        vtwo_alias_chunk<0, 0>(s0, s1, t, two, s2, tb, dA0, dA1, mA0, mA1, it, stop, first, active, on0, on1);
     } else if (wave_any(active && !on0))
       vtwo_chunk<0, 0, true>(s0, s1, t, two, sep, dA0, dA1, mA0, mA1, a1a0, a1b0, b1a0, b1b0, it, stop, first, active, on0,
                              on1);

@@ -193,18 +193,7 @@ int main(int argc, char **argv) {
             cf = all_s2 ? 2 : all_alias ? 2 : 1;
             cost = all_s2 && uniform ? 140 : all_alias ? 180 : 225;
           } else {
-            /* S3 family: every multi-contact lane is S3 or S2 ([01p*][s0p*]), at least one S3 */
-            int s3 = 0, other = 0;
-            for (int l = 0; l < 64; ++l) {
-              char key[64];
-              int live;
-              shape_key(&g_rec[w0 + l], t, key, &live);
-              if (live < 2) continue;
-              if (!strcmp(key, "[s0p1][10p1][s1p1]")) s3 = 1;
-              else if (!(live == 2 && !strncmp(key, "[01p", 4) && !strncmp(key + 6, "[s0p", 4))) other = 1;
-            }
-            s3 = s3 && !other;
-            (void)k;
+            const int s3 = uniform && !strcmp(k, "[s0p1][10p1][s1p1]") && nmulti > 0;
             cf = s3 ? 3 : 4; cost = s3 ? 190 : 109.0 * maxlive;
           }
           wf[cf] += cost * len;
