@@ -906,20 +906,21 @@ HK_DEV void vtwo_family(FSlot &s0, FSlot &s1, Dyn &B, bool two, int &it, bool &a
 // The tail's three-contact shape (r06, scripts/tail_shape_study.c): one island of three one-point contacts, slot 0
 // = (static, X), slot 1 = (Y, X), slot 2 = (static, Y) -- wall-puck, player-puck, wall-player -- optionally with
 // riders: one-contact lanes (their contact swapped into slot 0) and S2 two-contact lanes (player-puck, wall-player:
-// contact 0 in slot 0, contact 1 in slot 2; the slowest waves of the bench workload mostly hold S3 and S2 lanes
-// together).  X and Y live in locals, aliased at compile time, instead of the general family's body-file gathers
-// and scatters (~30 selects per contact): slot 0 runs the generic row on (A0, X) (a rider's own bodies; an S3 lane's
-// A0 is static, +0), slot 1 the dynamic row on (Y, X), whose update of X a non-S3 lane discards (one select per
-// component), slot 2 the static-body-A row on Y, which an S2 lane points at its body A0 (its contact 1's body B)
-// with one select per component before and after.  Non-S3 lanes' slot 1 impulses, and one-contact riders' slot 2
-// impulses, are restored at the end (another island's retired contacts may sit there).  The snapshot covers X, Y,
-// A0 and the three slots' impulses that the lane solves: the island's whole state, so the periodic exit stays exact;
-// this family starts its own chain.  Each lane's float operations are the general family's, in its order.  Runs
-// while some S3 lane iterates.
-template <int kP0, int kP2>
-HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, bool s2l, uint32_t mA0, bool dA0, f2 &vA0,
-                            float &wA0, f2 &vX, float &wX, f2 &vY, float &wY, uint32_t (&sn)[19], int &it, int stop,
-                            int first, bool &active) {
+// their live contacts swapped into slots 0 and 1, as the two-contact family holds them; the slowest waves of the
+// bench workload mostly hold S3 and S2 lanes together).  X and Y live in locals, aliased at compile time, instead of
+// the general family's body-file gathers and scatters (~30 selects per contact): slot 0 runs the generic row on
+// (A0, X) (a rider's own bodies; an S3 lane's A0 is static, +0), slot 1 the dynamic row on (Y, X) -- an S2 lane's
+// on (+0, A0), its static body A and its body B, contact 0's body A, by one select per component in and out (the
+// row with a +0 body A is bit-identical to the static-body-A row: see fslot_solve_velocity_p) -- whose update of X a
+// non-S3 lane discards, slot 2 the static-body-A row on Y, S3 lanes only in effect.  Non-S3 lanes' slot 2
+// impulses, and one-contact riders' slot 1 impulses, are restored at the end (another island's retired contacts may
+// sit there).  The snapshot covers X, Y, A0 and the impulses of the slots the lane solves: the island's whole
+// state, so the periodic exit stays exact; this family starts its own chain.  Each lane's float operations are the
+// general / two-contact families', in their order.  Runs while some S3 lane iterates.
+template <int kP0, int kP1>
+HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, bool s2l, uint32_t mA0, uint32_t mY, bool dA0,
+                            f2 &vA0, float &wA0, f2 &vX, float &wX, f2 &vY, float &wY, uint32_t (&sn)[19], int &it,
+                            int stop, int first, bool &active) {
   HK_MARK(vthree_begin);
   for (; it < stop && active; it += 4) {
 #pragma unroll
@@ -927,29 +928,29 @@ HK_DEV void vthree_s3_chunk(FSlot &s0, FSlot &s1, FSlot &s2, bool s3, bool s2l, 
       vA0 = f2{mask_f(vA0[0], mA0), mask_f(vA0[1], mA0)};  // static A (every S3 lane, static riders): +0
       wA0 = mask_f(wA0, mA0);
       fslot_solve_velocity_p<false, kP0>(s0, vA0, wA0, vX, wX);
-      f2 vB1 = vX;
-      float wB1 = wX;
-      fslot_solve_velocity_p<false, 1>(s1, vY, wY, vB1, wB1);
+      f2 vB1 = sel2(s2l, vA0, vX);  // an S2 lane's contact 1 acts on its body A0
+      float wB1 = s2l ? wA0 : wX;
+      vY = f2{mask_f(vY[0], mY), mask_f(vY[1], mY)};  // an S2 lane's contact 1 has a static body A: +0
+      wY = mask_f(wY, mY);
+      fslot_solve_velocity_p<false, kP1>(s1, vY, wY, vB1, wB1);
       vX = sel2(s3, vB1, vX);
       wX = s3 ? wB1 : wX;
-      vY = sel2(s2l, vA0, vY);  // an S2 lane's contact 1 acts on its body A0
-      wY = s2l ? wA0 : wY;
+      vA0 = sel2(s2l, vB1, vA0);
+      wA0 = s2l ? wB1 : wA0;
       f2 vA2 = f2{0.0f, 0.0f};
       float wA2 = 0.0f;
-      fslot_solve_velocity_p<true, kP2>(s2, vA2, wA2, vY, wY);
-      vA0 = sel2(s2l, vY, vA0);
-      wA0 = s2l ? wY : wA0;
+      fslot_solve_velocity_p<true, 1>(s2, vA2, wA2, vY, wY);
     }
-    const bool sl2 = s3 || s2l;  // lanes that solve slot 2
+    const bool sl1 = s3 || s2l;  // lanes that solve slot 1
     const uint32_t x[19] = {__float_as_uint(vX[0]), __float_as_uint(vX[1]), __float_as_uint(wX),
                             dA0 ? __float_as_uint(vA0[0]) : 0u, dA0 ? __float_as_uint(vA0[1]) : 0u,
                             dA0 ? __float_as_uint(wA0) : 0u, __float_as_uint(s0.ni[0]), __float_as_uint(s0.ni[1]),
                             __float_as_uint(s0.ti[0]), __float_as_uint(s0.ti[1]),
                             s3 ? __float_as_uint(vY[0]) : 0u, s3 ? __float_as_uint(vY[1]) : 0u,
-                            s3 ? __float_as_uint(wY) : 0u, s3 ? __float_as_uint(s1.ni[0]) : 0u,
-                            s3 ? __float_as_uint(s1.ti[0]) : 0u, sl2 ? __float_as_uint(s2.ni[0]) : 0u,
-                            sl2 ? __float_as_uint(s2.ti[0]) : 0u, sl2 ? __float_as_uint(s2.ni[1]) : 0u,
-                            sl2 ? __float_as_uint(s2.ti[1]) : 0u};
+                            s3 ? __float_as_uint(wY) : 0u, sl1 ? __float_as_uint(s1.ni[0]) : 0u,
+                            sl1 ? __float_as_uint(s1.ti[0]) : 0u, sl1 ? __float_as_uint(s1.ni[1]) : 0u,
+                            sl1 ? __float_as_uint(s1.ti[1]) : 0u, s3 ? __float_as_uint(s2.ni[0]) : 0u,
+                            s3 ? __float_as_uint(s2.ti[0]) : 0u};
     uint32_t d = 0u;
 #pragma unroll
     for (int k = 0; k < 19; ++k) {
@@ -970,14 +971,13 @@ HK_DEV bool s2_bits(int bits0, int bits1) {
   const int a0 = (bits0 >> 7) & 15, a1 = (bits1 >> 7) & 15, b1 = (bits1 >> 11) & 15;
   return a1 >= 3 && b1 == a0 && ((bits0 >> 5) & 3) == ((bits1 >> 5) & 3);
 }
-// s3: an S3 lane; s2l: an S2 lane (contact 0 in slot 0, contact 1 in slot 2); else a one-contact rider (slot 0)
+// s3: an S3 lane; s2l: an S2 lane (its contacts in slots 0 and 1); else a one-contact rider (slot 0)
 HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, bool s2l, int &it, bool &active,
                              int first) {
   const bool entered = active;
   const int a0 = fs_bA(s0), x = fs_bB(s0), y = s3 ? fs_bA(s1) : x;
   const bool dA0 = a0 < 3;
-  const uint32_t mA0 = lane_mask(dA0);
-  const int vc0 = fs_vcount(s0), vc2 = s2l ? fs_vcount(s2) : 1;
+  const uint32_t mA0 = lane_mask(dA0), mY = lane_mask(s3);
   v2 q;
   float wA0, wX, wY;
   get_vel_a(B, a0, q, wA0);
@@ -993,26 +993,22 @@ HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, b
   for (int k = 0; k < 19; ++k) sn[k] = 0u;
   while (wave_any(active && s3)) {
     const int stop = chunk_end(it);
-    const bool p0 = !wave_any(active && vc0 != 1), p2 = !wave_any(active && vc2 != 1);
-    if (p0 && p2)
-      vthree_s3_chunk<1, 1>(s0, s1, s2, s3, s2l, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
-    else if (p2)
-      vthree_s3_chunk<0, 1>(s0, s1, s2, s3, s2l, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
-    else
-      vthree_s3_chunk<0, 0>(s0, s1, s2, s3, s2l, mA0, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+    // one variant, per-lane point counts: a second, one-point variant made the kernel spill (the chunk's invariants
+    // hoisted for both; 16 -> 152 B of scratch per lane, 0 -> 33 spilled VGPRs, make resource-usage)
+    vthree_s3_chunk<0, 0>(s0, s1, s2, s3, s2l, mA0, mY, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
   }
   if (entered) {
     if (dA0) set_vel_a(B, a0, V2(vA0), wA0);
     set_vel_b(B, x, V2(vX), wX);
     if (s3) set_vel_b(B, y, V2(vY), wY);
   }
-  const bool sl2 = s3 || s2l;
+  const bool sl1 = s3 || s2l;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    s1.ni[j] = s3 ? s1.ni[j] : ni1[j];
-    s1.ti[j] = s3 ? s1.ti[j] : ti1[j];
-    s2.ni[j] = sl2 ? s2.ni[j] : ni2[j];
-    s2.ti[j] = sl2 ? s2.ti[j] : ti2[j];
+    s1.ni[j] = sl1 ? s1.ni[j] : ni1[j];
+    s1.ti[j] = sl1 ? s1.ti[j] : ti1[j];
+    s2.ni[j] = s3 ? s2.ni[j] : ni2[j];
+    s2.ti[j] = s3 ? s2.ti[j] : ti2[j];
   }
 }
 
@@ -1145,22 +1141,16 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3], Ph
       }
       if (s3ok) {
         if constexpr (SlotCap<SL>::value >= 3) {
-          // riders' and S2 lanes' contact 0 to slot 0; an S2 lane's contact 1 to slot 2 (j0 < j1, so the first swap
-          // leaves j1 in place)
-          const bool mv0 = !s3 && j0 != 0, mv12 = s2l && j1 == 1;
-          const bool mv23 = SlotCap<SL>::value >= 4 && s2l && j1 == 3;
-          const bool any0 = wave_any(active && mv0), any12 = wave_any(mv12), any23 = wave_any(mv23);
+          // riders' and S2 lanes' live contacts to slots 0 (and 1), in slot order, as the two-contact family has them
+          const bool mv0 = !s3 && j0 != 0, mv1 = s2l && j1 != 1;
+          const bool any0 = wave_any(active && mv0), any1 = wave_any(mv1);
           if (any0) slot_swap(S, 0, mv0 ? j0 : 0);
-          if (any12) slot_swap(S, 1, mv12 ? 2 : 1);
-          if constexpr (SlotCap<SL>::value >= 4)
-            if (any23) slot_swap(S, 2, mv23 ? 3 : 2);
+          if (any1) slot_swap(S, 1, mv1 ? j1 : 1);
           const bool entered = active;
           if (s3) HK_HOST_DIAG_INC(2);
           vthree_s3_family(S.s[0], S.s[1], S.s[2], B, s3, s2l, it, active, first);
           live = entered && !active ? 0u : live;
-          if constexpr (SlotCap<SL>::value >= 4)
-            if (any23) slot_swap(S, 2, mv23 ? 3 : 2);
-          if (any12) slot_swap(S, 1, mv12 ? 2 : 1);
+          if (any1) slot_swap(S, 1, mv1 ? j1 : 1);
           if (any0) slot_swap(S, 0, mv0 ? j0 : 0);
           HK_FAM_ADD(T, 0);
         }

@@ -108,6 +108,55 @@ __device__ __forceinline__ void gemm256_ahead(const f4 *__restrict__ P, Tile &in
   }
 }
 
+// candidate (r06): no LDS staging and no workgroup barrier -- every wave loads its own A fragments from L2 / L1 (the
+// workgroup's 4 waves read the same lines, so 3 of 4 hit L1), half a k-block (8 output blocks) at a time, the next
+// half's 8 loads in flight while this half's 32 MFMAs run (8 independent accumulators)
+__device__ __forceinline__ void gemm256_direct(const f4 *__restrict__ P, Tile &in, const float *__restrict__ bias,
+                                               Tile &out, int lane) {
+  const int q = lane >> 4;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) out.v[ob] = z4();
+  f4 a[2][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[0][i] = P[(i * 16) * 64 + lane];
+#pragma unroll
+  for (int h = 0; h < 32; ++h) {
+    const int kb = h >> 1, ob0 = (h & 1) * 8;
+    if (h + 1 < 32) {
+      const int kb1 = (h + 1) >> 1, ob1 = ((h + 1) & 1) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[(h + 1) & 1][i] = P[((ob1 + i) * 16 + kb1) * 64 + lane];
+    }
+    if (bias && (h & 1) == 0) {
+      const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * kb + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) in.v[kb][r] = tanh_fast(in.v[kb][r] + bb[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float b = in.v[kb][r];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) out.v[ob0 + i] = mfma(a[h & 1][i][r], b, out.v[ob0 + i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the next halves' loads from being hoisted (registers)
+  }
+}
+__global__ void __launch_bounds__(WG, 1) gemm_direct_kernel(const f4 *P, const float *bias, float *out, int reps) {
+  const int lane = threadIdx.x & 63;
+  Tile a, b;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) a.v[ob] = f4{0.01f * lane, 0.02f, 0.03f, 0.04f * ob};
+  for (int r = 0; r < 2 * reps; ++r) {
+    gemm256_direct(P, a, bias, b, lane);
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) a.v[ob] = b.v[ob];
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) s += a.v[ob][0] + a.v[ob][1] + a.v[ob][2] + a.v[ob][3];
+  out[blockIdx.x * WG + threadIdx.x] = s;
+}
+
 template <int kV>
 __global__ void __launch_bounds__(WG, 1) gemm_var3_kernel(const f4 *P, const float *bias, float *out, int reps) {
   __shared__ f4 sfrag[3 * 16 * 64 + 64];
@@ -181,10 +230,10 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int tb = 0; tb < 4; ++tb)
+  for (int tb = 0; tb < 5; ++tb)
   for (int reps : {4, 8}) {
-    auto kern = tb == 1 ? gemm_var_kernel<true> : tb == 0 ? gemm_var_kernel<false> : tb == 2 ? gemm_var3_kernel<2>
-                                                                                          : gemm_var3_kernel<3>;
+    auto kern = tb == 4 ? gemm_direct_kernel : tb == 1 ? gemm_var_kernel<true> : tb == 0 ? gemm_var_kernel<false>
+                : tb == 2 ? gemm_var3_kernel<2> : gemm_var3_kernel<3>;
     hipLaunchKernelGGL(kern, dim3(256), dim3(WG), 0, 0, P, bias, out, reps);
     hipEventRecord(e0);
     for (int k = 0; k < 20; ++k) hipLaunchKernelGGL(kern, dim3(256), dim3(WG), 0, 0, P, bias, out, reps);
@@ -195,7 +244,8 @@ int main() {
     const double us = ms * 1e3 / 20, calls = 2.0 * reps;
     const double flop = calls * 2.0 * 256 * 256 * 16384;  // per launch
     printf("%s gemm256 x %d per wave: %.1f us per launch, %.2f us per gemm256 call, %.1f TFLOP/s\n",
-           tb == 1 ? "triple-buffered" : tb == 0 ? "current" : tb == 2 ? "tanh-ahead" : "no-activation", (int)calls, us,
+           tb == 4 ? "direct (r06)" : tb == 1 ? "triple-buffered" : tb == 0 ? "current" : tb == 2 ? "tanh-ahead"
+                                                                                         : "no-activation", (int)calls, us,
            us / calls, flop / (us * 1e-6) / 1e12);
     (void)0;
   }
