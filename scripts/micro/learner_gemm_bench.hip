@@ -111,9 +111,11 @@ __device__ __forceinline__ void gemm256_ahead(const f4 *__restrict__ P, Tile &in
 // candidate (r06): no LDS staging and no workgroup barrier -- every wave loads its own A fragments from L2 / L1 (the
 // workgroup's 4 waves read the same lines, so 3 of 4 hit L1), half a k-block (8 output blocks) at a time, the next
 // half's 8 loads in flight while this half's 32 MFMAs run (8 independent accumulators)
-__device__ __forceinline__ void gemm256_direct(const f4 *__restrict__ P, Tile &in, const float *__restrict__ bias,
+__device__ __forceinline__ void gemm256_direct(const f4 *__restrict__ P0, Tile &in, const float *__restrict__ bias,
                                                Tile &out, int lane) {
   const int q = lane >> 4;
+  const f4 *P = P0;
+  asm volatile("" : "+s"(P));  // a fresh operand per call, as in the kernels (no loads hoisted out of a caller's loop)
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) out.v[ob] = z4();
   f4 a[2][8];
@@ -140,6 +142,52 @@ __device__ __forceinline__ void gemm256_direct(const f4 *__restrict__ P, Tile &i
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the next halves' loads from being hoisted (registers)
   }
+}
+// the same with whole k-blocks: the next block's 16 fragment loads in flight during this block's 64 MFMAs
+__device__ __forceinline__ void gemm256_direct16(const f4 *__restrict__ P0, Tile &in, const float *__restrict__ bias,
+                                                 Tile &out, int lane) {
+  const int q = lane >> 4;
+  const f4 *P = P0;
+  asm volatile("" : "+s"(P));
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) out.v[ob] = z4();
+  f4 a[2][16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[0][i] = P[(i * 16) * 64 + lane];
+#pragma unroll
+  for (int kb = 0; kb < 16; ++kb) {
+    if (kb + 1 < 16) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) a[(kb + 1) & 1][i] = P[(i * 16 + kb + 1) * 64 + lane];
+    }
+    if (bias) {
+      const f4 bb = *reinterpret_cast<const f4 *>(bias + 16 * kb + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) in.v[kb][r] = tanh_fast(in.v[kb][r] + bb[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float b = in.v[kb][r];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) out.v[i] = mfma(a[kb & 1][i][r], b, out.v[i]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+__global__ void __launch_bounds__(WG, 1) gemm_direct16_kernel(const f4 *P, const float *bias, float *out, int reps) {
+  const int lane = threadIdx.x & 63;
+  Tile a, b;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) a.v[ob] = f4{0.01f * lane, 0.02f, 0.03f, 0.04f * ob};
+  for (int r = 0; r < 2 * reps; ++r) {
+    gemm256_direct16(P, a, bias, b, lane);
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) a.v[ob] = b.v[ob];
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) s += a.v[ob][0] + a.v[ob][1] + a.v[ob][2] + a.v[ob][3];
+  out[blockIdx.x * WG + threadIdx.x] = s;
 }
 __global__ void __launch_bounds__(WG, 1) gemm_direct_kernel(const f4 *P, const float *bias, float *out, int reps) {
   const int lane = threadIdx.x & 63;
@@ -230,9 +278,9 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int tb = 0; tb < 5; ++tb)
+  for (int tb = 0; tb < 6; ++tb)
   for (int reps : {4, 8}) {
-    auto kern = tb == 4 ? gemm_direct_kernel : tb == 1 ? gemm_var_kernel<true> : tb == 0 ? gemm_var_kernel<false>
+    auto kern = tb == 5 ? gemm_direct16_kernel : tb == 4 ? gemm_direct_kernel : tb == 1 ? gemm_var_kernel<true> : tb == 0 ? gemm_var_kernel<false>
                 : tb == 2 ? gemm_var3_kernel<2> : gemm_var3_kernel<3>;
     hipLaunchKernelGGL(kern, dim3(256), dim3(WG), 0, 0, P, bias, out, reps);
     hipEventRecord(e0);
@@ -244,7 +292,7 @@ int main() {
     const double us = ms * 1e3 / 20, calls = 2.0 * reps;
     const double flop = calls * 2.0 * 256 * 256 * 16384;  // per launch
     printf("%s gemm256 x %d per wave: %.1f us per launch, %.2f us per gemm256 call, %.1f TFLOP/s\n",
-           tb == 4 ? "direct (r06)" : tb == 1 ? "triple-buffered" : tb == 0 ? "current" : tb == 2 ? "tanh-ahead"
+           tb == 5 ? "direct, whole blocks (r06)" : tb == 4 ? "direct, half blocks (r06)" : tb == 1 ? "triple-buffered" : tb == 0 ? "current" : tb == 2 ? "tanh-ahead"
                                                                                          : "no-activation", (int)calls, us,
            us / calls, flop / (us * 1e-6) / 1e12);
     (void)0;
