@@ -25,9 +25,24 @@ def _run(script, *args):
 
 
 def test_noise_study_summary_regenerates():
+    """r06's summary (profiles/r06/noise_study_summary_t.json: r05's plus the Welch-Satterthwaite df and t-based p per
+    cell) regenerates from r05's run records, and every number r05's committed summary holds is unchanged."""
     got = _run("noise_study_summary.py", os.path.join("profiles", "r05", "noise_runs"))
-    want = json.load(open(os.path.join(R05, "noise_study_summary.json")))
+    want = json.load(open(os.path.join(ROOT, "profiles", "r06", "noise_study_summary_t.json")))
     assert got == want
+    old = json.load(open(os.path.join(R05, "noise_study_summary.json")))
+    for proto, cells in old["protocols"].items():
+        for cell, row in cells.items():
+            for key, v in row.items():
+                if isinstance(v, dict):
+                    assert {k: got["protocols"][proto][cell][key][k] for k in v} == v, (proto, cell, key)
+                else:
+                    assert got["protocols"][proto][cell][key] == v, (proto, cell, key)
+    for proto, cells in got["protocols"].items():
+        for cell, row in cells.items():
+            for key in ("wr_weak", "wr_strong"):
+                assert row[key]["welch_df"] is None or row[key]["welch_df"] > 1.0
+                assert row[key]["welch_p"] is None or 0.0 <= row[key]["welch_p"] <= 1.0
 
 
 @pytest.mark.parametrize("ref", ["stage1", "stage2", "sp_per", "scratch_ou"])
