@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include "../../include/hockey.h"
@@ -176,7 +177,7 @@ int hk_create(int device, int64_t n, const hk_config *cfg, void **out) {
   c->cfg.arena_offset = cfg->arena_offset;
   c->cfg.diag = cfg->diag_flags;
   c->s.n = n;
-  const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NIF * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
+  const size_t nf = (size_t)hk::NFF * n, ni = (size_t)hk::NPW * n, nm = (size_t)hk::NSOLID * hk::NMF * n;
   const size_t nw = (size_t)hk::workspace_words_per_arena() * n;
   if ((e = hipMalloc(&c->s.f, nf * 4)) != hipSuccess || (e = hipMalloc(&c->s.i, ni * 4)) != hipSuccess ||
       (e = hipMalloc(&c->s.man, nm * 4)) != hipSuccess || (e = hipMalloc(&c->s.phase, 3 * n * 8)) != hipSuccess ||
@@ -233,12 +234,44 @@ int hk_set_policy(void *ctx, int player, int policy) {
   return HK_OK;
 }
 
+// The packed int words (hk_kernels.h PW_*) hold has_puck in [0, 255], max_t in [0, 65535], done in {0, 1} and
+// winner in {-1, 0, 1}: a caller's per-arena values outside those ranges are rejected before anything is launched
+// (HK_E_INVALID).  The arrays are device memory; they are copied to the host on the call's stream for the check
+// (reset / set_state are not on the step path).  Only arenas the mask selects are checked.
+static int check_ints(const char *who, int64_t n, int cols, const int32_t *dev, const uint8_t *mask_dev,
+                      hipStream_t st) {
+  std::vector<int32_t> v((size_t)n * cols);
+  std::vector<uint8_t> m(mask_dev ? (size_t)n : 0);
+  hipError_t e = hipMemcpyAsync(v.data(), dev, v.size() * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && mask_dev) e = hipMemcpyAsync(m.data(), mask_dev, m.size(), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hipfail(e, who);
+  for (int64_t a = 0; a < n; ++a) {
+    if (mask_dev && !m[a]) continue;
+    const int32_t *r = v.data() + a * cols;
+    if (cols == 1) {
+      if (r[0] < 0 || r[0] > hk::kMaxTMax)
+        return fail(HK_E_INVALID, "%s: max_t out of range [0, 65535]", who);
+      continue;
+    }
+    if (r[0] < 0 || r[0] > hk::kHasMax || r[1] < 0 || r[1] > hk::kHasMax)
+      return fail(HK_E_INVALID, "%s: aux has_puck out of range [0, 255]", who);
+    if (r[3] < 0 || r[3] > 1) return fail(HK_E_INVALID, "%s: aux done not 0 or 1", who);
+    if (r[4] < -1 || r[4] > 1) return fail(HK_E_INVALID, "%s: aux winner not -1, 0 or 1", who);
+  }
+  return HK_OK;
+}
+
 int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t *max_t, const uint8_t *one_starts,
              void *stream) {
   if (!ctx) return fail(HK_E_INVALID, "hk_reset: ctx is NULL%s");
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
   HK_QUIESCE(c, "hk_reset");
+  if (max_t) {
+    const int rc = check_ints("hk_reset", c->s.n, 1, max_t, mask, (hipStream_t)stream);
+    if (rc != HK_OK) return rc;
+  }
   hipError_t e = hk::launch_reset(c->s, c->cfg, mask, params, max_t, one_starts, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_reset");
 }
@@ -479,6 +512,10 @@ int hk_set_state(void *ctx, const uint8_t *mask, const float *state, const int32
   Ctx *c = (Ctx *)ctx;
   DeviceGuard g(c->device);
   HK_QUIESCE(c, "hk_set_state");
+  if (aux) {
+    const int rc = check_ints("hk_set_state", c->s.n, 5, aux, mask, (hipStream_t)stream);
+    if (rc != HK_OK) return rc;
+  }
   hipError_t e = hk::launch_set_state(c->s, c->cfg, mask, state, aux, (hipStream_t)stream);
   return e == hipSuccess ? HK_OK : hipfail(e, "hk_set_state");
 }
@@ -564,8 +601,8 @@ int hk_bytes_per_step(const void *ctx, int64_t *algorithmic, int64_t *implementa
   // scalars 16 B, obs 72 B, reward 4 B, done 1 B written = 285 B per env-step.
   if (algorithmic) *algorithmic = 285;
   // implementation (excluding manifolds, which are only touched where a pair is in contact):
-  // f: 29 floats read+write, i: 12 ints read+write, obs 72 + reward 4 + done 1 + info 16.
-  if (implementation) *implementation = (int64_t)(hk::NFF * 4 * 2 + hk::NIF * 4 * 2 + 72 + 4 + 1 + 16);
+  // f: 29 floats read+write, i: 6 packed int words read+write (r06; 12 before), obs 72 + reward 4 + done 1 + info 16.
+  if (implementation) *implementation = (int64_t)(hk::NFF * 4 * 2 + hk::NPW * 4 * 2 + 72 + 4 + 1 + 16);
   return HK_OK;
 }
 

@@ -10,8 +10,40 @@ namespace hk {
 // per dynamic body float fields (f[b*FB + k][N])
 enum { FB_PX = 0, FB_PY, FB_CX, FB_CY, FB_A, FB_VX, FB_VY, FB_W, FB_SLEEP, FB };
 enum { F_PFX = 3 * FB, F_PFY, NFF };
-// int fields
+// int fields: the 12 logical words a lane works with (registers) ...
 enum { I_AWAKE = 0, I_HAS1, I_HAS2, I_TIME, I_DONE, I_WINNER, I_MAXT, I_TOUCH, I_ENABLED, I_ONE, I_EPISODE, I_STEP, NIF };
+// ... and the 6 packed words they live in in HBM (r06, VERDICT r05 item 6: 48 -> 24 B read per arena-step):
+//   PW_TAW  touching mask (27 pairs) | awake bits << 27 | done << 30 | one_starts << 31
+//   PW_ENW  enabled mask (27 pairs) | (winner + 1) << 27
+//   PW_HM   has_puck1 | has_puck2 << 8 | max_t << 16       (has_puck in [0, 255], max_t in [0, 65535])
+//   PW_TIME, PW_EPISODE, PW_STEP: whole words
+// hk_set_state / hk_reset reject aux / max_t values outside these ranges with HK_E_INVALID (include/hockey.h).
+enum { PW_TAW = 0, PW_ENW, PW_HM, PW_TIME, PW_EPISODE, PW_STEP, NPW };
+constexpr int kHasMax = 255, kMaxTMax = 65535;
+HK_DEV void unpack_ints(const uint32_t (&p)[NPW], int32_t (&iw)[NIF]) {
+  iw[I_TOUCH] = (int32_t)(p[PW_TAW] & 0x07ffffffu);
+  iw[I_AWAKE] = (int32_t)((p[PW_TAW] >> 27) & 7u);
+  iw[I_DONE] = (int32_t)((p[PW_TAW] >> 30) & 1u);
+  iw[I_ONE] = (int32_t)(p[PW_TAW] >> 31);
+  iw[I_ENABLED] = (int32_t)(p[PW_ENW] & 0x07ffffffu);
+  iw[I_WINNER] = (int32_t)((p[PW_ENW] >> 27) & 3u) - 1;
+  iw[I_HAS1] = (int32_t)(p[PW_HM] & 0xffu);
+  iw[I_HAS2] = (int32_t)((p[PW_HM] >> 8) & 0xffu);
+  iw[I_MAXT] = (int32_t)(p[PW_HM] >> 16);
+  iw[I_TIME] = (int32_t)p[PW_TIME];
+  iw[I_EPISODE] = (int32_t)p[PW_EPISODE];
+  iw[I_STEP] = (int32_t)p[PW_STEP];
+}
+HK_DEV void pack_ints(const int32_t (&iw)[NIF], uint32_t (&p)[NPW]) {
+  p[PW_TAW] = ((uint32_t)iw[I_TOUCH] & 0x07ffffffu) | (((uint32_t)iw[I_AWAKE] & 7u) << 27) |
+              (((uint32_t)iw[I_DONE] & 1u) << 30) | (((uint32_t)iw[I_ONE] & 1u) << 31);
+  p[PW_ENW] = ((uint32_t)iw[I_ENABLED] & 0x07ffffffu) | (((uint32_t)(iw[I_WINNER] + 1) & 3u) << 27);
+  p[PW_HM] = ((uint32_t)iw[I_HAS1] & 0xffu) | (((uint32_t)iw[I_HAS2] & 0xffu) << 8) |
+             (((uint32_t)iw[I_MAXT] & 0xffffu) << 16);
+  p[PW_TIME] = (uint32_t)iw[I_TIME];
+  p[PW_EPISODE] = (uint32_t)iw[I_EPISODE];
+  p[PW_STEP] = (uint32_t)iw[I_STEP];
+}
 // manifold record per (solid pair, arena): 16 words = 64 B, read / written as four 16-B quads
 //   q0 {meta, local normal x, y, local point x}   q1 {local point y, point0 x, y, point1 x}
 //   q2 {point1 y, id0, id1, pad}                  q3 {normal impulse 0, tangent impulse 0, normal 1, tangent 1}
@@ -21,7 +53,7 @@ static_assert(NMF == 16, "a manifold record is four 16-byte quads");
 
 struct DevState {
   float *f;
-  int32_t *i;
+  int32_t *i;  // packed int words [NPW][N] (PW_*)
   float *man;  // manifold records [NSOLID][N][NMF] (64 B per record, hk_arena.h ManRec)
   float *ws;  // large-island slot workspace [kBigC][kSlotWords][N] (hk_solver.h HbmSlots)
   double *phase;  // BasicOpponent phases [3][N]: player 1, player 2 (its policy / the strong bot under a

@@ -5,8 +5,9 @@
 // of every field):
 //   f[NFF][N]            float  body state: per dynamic body {origin x,y, COM x,y, angle, vx, vy, w,
 //                               sleep time} + the puck's pending force (TRAIN_DEFENSE reset)
-//   i[NIF][N]            int32  awake bits, has_puck1/2, time, done, winner, max_t, touching mask,
-//                               enabled mask, one_starts, episode and step counters
+//   i[NPW][N]            int32  the packed int words (hk_kernels.h PW_*): touching mask | awake | done |
+//                               one_starts, enabled mask | winner, has_puck1 | has_puck2 | max_t, time,
+//                               episode and step counters (the 12 logical words I_* live in registers)
 //   man[NSOLID][N][NMF]  float  Box2D manifold record (64 B) of every solid pair (read/written in place,
 //                               touching only; hk_arena.h man_rec)
 //   phase[3][N]          double BasicOpponent phases: player 1, player 2, player 2's weak bot under a per-arena
@@ -44,14 +45,23 @@ enum { RNG_ACTION = 1, RNG_PHASE = 2, RNG_RESET = 3, RNG_PHASE0 = 4 };
 // world <-> HBM
 // ------------------------------------------------------------------------------------------------
 HK_DEV float &F(const DevState &s, int field, int64_t a) { return s.f[(int64_t)field * s.n + a]; }
-HK_DEV int32_t &I(const DevState &s, int field, int64_t a) { return s.i[(int64_t)field * s.n + a]; }
+// packed int word k (PW_*) of arena a
+HK_DEV uint32_t &PW(const DevState &s, int k, int64_t a) {
+  return reinterpret_cast<uint32_t *>(s.i)[(int64_t)k * s.n + a];
+}
+HK_DEV void load_ints(const DevState &s, int64_t a, uint32_t (&pw)[NPW], int32_t (&iw)[NIF]) {
+#pragma unroll
+  for (int k = 0; k < NPW; ++k) pw[k] = PW(s, k, a);
+  unpack_ints(pw, iw);
+}
 
 // The HBM words one arena's step reads before it computes anything: its state, the acting BasicOpponents'
 // phases, the per-arena policy override, phase increments and external actions.  step_kernel issues these
 // loads before its scene copy, so the whole fetch costs one memory latency instead of one per dependent use.
 struct StepWords {
   float f[NFF];
-  int32_t i[NIF];
+  uint32_t pw[NPW];  // the packed int words as fetched
+  int32_t i[NIF];    // ... unpacked
   double ph[3];
   double inc[2];
   float act[8];
@@ -61,7 +71,8 @@ HK_DEV void fetch_words(StepWords &m, const DevState &s, const KCfg &cfg, const 
 #pragma unroll
   for (int k = 0; k < NFF; ++k) m.f[k] = F(s, k, a);
 #pragma unroll
-  for (int k = 0; k < NIF; ++k) m.i[k] = I(s, k, a);
+  for (int k = 0; k < NPW; ++k) m.pw[k] = PW(s, k, a);
+  unpack_ints(m.pw, m.i);
   // phase rows a bot may use (wave-uniform conditions; row 2 only under an override)
   m.ph[0] = cfg.policy[0] >= 2 ? s.phase[a] : 0.0;
   m.ph[1] = (cfg.policy[1] >= 2 || io.policy2) ? s.phase[s.n + a] : 0.0;
@@ -135,15 +146,31 @@ HK_DEV void unpack_arena(Arena &w, const float *fw, const int32_t *iw, int64_t a
 }
 HK_DEV void load_arena(Arena &w, const DevState &s, int64_t a, int keep_mode, int vel_ref, float *lds, int lane) {
   float fw[NFF];
+  uint32_t pw[NPW];
   int32_t iw[NIF];
 #pragma unroll
   for (int k = 0; k < NFF; ++k) fw[k] = F(s, k, a);
-#pragma unroll
-  for (int k = 0; k < NIF; ++k) iw[k] = I(s, k, a);
+  load_ints(s, a, pw, iw);
   unpack_arena(w, fw, iw, a, s, keep_mode, vel_ref, lds, lane);
 }
 
-HK_DEV void store_arena(const Arena &w, const DevState &s, int64_t a) {
+// the logical int words of an arena after a step / reset (one_starts, episode and step passed in)
+HK_DEV void arena_ints(const Arena &w, int awake, int one, int ep, int step, int32_t (&iw)[NIF]) {
+  iw[I_AWAKE] = awake;
+  iw[I_HAS1] = w.has1;
+  iw[I_HAS2] = w.has2;
+  iw[I_TIME] = w.time;
+  iw[I_DONE] = w.done;
+  iw[I_WINNER] = w.winner;
+  iw[I_MAXT] = w.max_t;
+  iw[I_TOUCH] = (int)w.touch;
+  iw[I_ENABLED] = (int)w.enabled;
+  iw[I_ONE] = one;
+  iw[I_EPISODE] = ep;
+  iw[I_STEP] = step;
+}
+// one < 0: keep the stored one_starts bit
+HK_DEV void store_arena(const Arena &w, const DevState &s, int64_t a, int one = -1) {
   int awake = 0;
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
@@ -161,22 +188,24 @@ HK_DEV void store_arena(const Arena &w, const DevState &s, int64_t a) {
   }
   F(s, F_PFX, a) = w.d.fx[B_PK];
   F(s, F_PFY, a) = w.d.fy[B_PK];
-  I(s, I_AWAKE, a) = awake;
-  I(s, I_HAS1, a) = w.has1;
-  I(s, I_HAS2, a) = w.has2;
-  I(s, I_TIME, a) = w.time;
-  I(s, I_DONE, a) = w.done;
-  I(s, I_WINNER, a) = w.winner;
-  I(s, I_MAXT, a) = w.max_t;
-  I(s, I_TOUCH, a) = (int)w.touch;
-  I(s, I_ENABLED, a) = (int)w.enabled;
+  if (one < 0) one = (int)(PW(s, PW_TAW, a) >> 31);
+  int32_t iw[NIF];
+  uint32_t pw[NPW];
+  arena_ints(w, awake, one, 0, 0, iw);
+  pack_ints(iw, pw);
+  PW(s, PW_TAW, a) = pw[PW_TAW];
+  PW(s, PW_ENW, a) = pw[PW_ENW];
+  PW(s, PW_HM, a) = pw[PW_HM];
+  PW(s, PW_TIME, a) = pw[PW_TIME];
 }
 
 // store_arena after a step: the same words, but the fields that rarely change in play (sleep times, the puck's
 // pending force, awake bits, has_puck, done, winner, time limit, touching / enabled masks) are written only by
 // lanes whose value changed against the step's fetched words (fw, iw).  A wave whose 16 lanes of a 64-B segment
 // all keep their value issues no write for it, which takes those fields off the HBM write traffic.
-HK_DEV void store_arena_changed(const Arena &w, const DevState &s, int64_t a, const float *fw, const int32_t *iw) {
+// one / ep / step: the arena's one_starts, episode and step words after this step
+HK_DEV void store_arena_changed(const Arena &w, const DevState &s, int64_t a, const float *fw, const uint32_t *pw0,
+                                int one, int ep, int step) {
   int awake = 0;
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
@@ -194,15 +223,15 @@ HK_DEV void store_arena_changed(const Arena &w, const DevState &s, int64_t a, co
   }
   if (__float_as_uint(w.d.fx[B_PK]) != __float_as_uint(fw[F_PFX])) F(s, F_PFX, a) = w.d.fx[B_PK];
   if (__float_as_uint(w.d.fy[B_PK]) != __float_as_uint(fw[F_PFY])) F(s, F_PFY, a) = w.d.fy[B_PK];
-  if (awake != iw[I_AWAKE]) I(s, I_AWAKE, a) = awake;
-  if (w.has1 != iw[I_HAS1]) I(s, I_HAS1, a) = w.has1;
-  if (w.has2 != iw[I_HAS2]) I(s, I_HAS2, a) = w.has2;
-  I(s, I_TIME, a) = w.time;
-  if (w.done != iw[I_DONE]) I(s, I_DONE, a) = w.done;
-  if (w.winner != iw[I_WINNER]) I(s, I_WINNER, a) = w.winner;
-  if (w.max_t != iw[I_MAXT]) I(s, I_MAXT, a) = w.max_t;
-  if ((int)w.touch != iw[I_TOUCH]) I(s, I_TOUCH, a) = (int)w.touch;
-  if ((int)w.enabled != iw[I_ENABLED]) I(s, I_ENABLED, a) = (int)w.enabled;
+  int32_t iw[NIF];
+  uint32_t pw[NPW];
+  arena_ints(w, awake, one, ep, step, iw);
+  pack_ints(iw, pw);
+  PW(s, PW_TIME, a) = pw[PW_TIME];
+  PW(s, PW_STEP, a) = pw[PW_STEP];
+#pragma unroll
+  for (int k = 0; k < NPW; ++k)
+    if (k != PW_TIME && k != PW_STEP && pw[k] != pw0[k]) PW(s, k, a) = pw[k];
 }
 
 // HockeyEnv.reset body re-creation (hockey_env.py:345-418) from placement params.
@@ -331,21 +360,23 @@ HK_DEV void reset_lane(const DevState &s, const KCfg &cfg, int64_t a, const floa
   load_arena(w, s, a, cfg.keep_mode, cfg.vel_ref, nullptr, 0);
   float p6[6];
   int mt;
-  int one = I(s, I_ONE, a);
+  uint32_t pw[NPW];
+  int32_t iw[NIF];
+  load_ints(s, a, pw, iw);
+  int one = iw[I_ONE];
   if (params) {
     for (int k = 0; k < 6; ++k) p6[k] = params[a * 6 + k];
     mt = cfg.mode == 0 ? 250 : 80;
     if (cfg.mode == 0) one = one_in ? (int)one_in[a] : !one;
   } else {
     if (cfg.mode == 0) one = one_in ? (int)one_in[a] : !one;
-    const uint32_t ep = (uint32_t)I(s, I_EPISODE, a);
+    const uint32_t ep = (uint32_t)iw[I_EPISODE];
     device_placement(cfg.seed, cfg.arena_offset + a, ep, cfg.mode, one, p6, mt);
   }
   if (max_t_in) mt = max_t_in[a];
   reset_arena(w, p6, mt);
-  store_arena(w, s, a);
-  I(s, I_ONE, a) = one;
-  I(s, I_EPISODE, a) = I(s, I_EPISODE, a) + 1;
+  store_arena(w, s, a, one);
+  PW(s, PW_EPISODE, a) = (uint32_t)iw[I_EPISODE] + 1u;
 }
 
 // One HockeyEnv.step of arena a (policy actions, pre-solve laws, world.Step, outputs, then auto-reset).
@@ -465,16 +496,17 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     rec[15] = 0.0;
   }
   const int done_edge = !was_done && w.done, winner = w.winner;
+  int one_new = m.i[I_ONE], ep_new = m.i[I_EPISODE];
   if (cfg.auto_reset && w.done) {  // the next episode starts now; obs / obs2 describe its first state
-    int one = I(s, I_ONE, a);
+    int one = m.i[I_ONE];
     if (cfg.mode == 0) one = !one;
-    const uint32_t ep = (uint32_t)I(s, I_EPISODE, a);
+    const uint32_t ep = (uint32_t)m.i[I_EPISODE];
     float p6[6];
     int mt;
     device_placement(cfg.seed, cfg.arena_offset + a, ep, cfg.mode, one, p6, mt);
     reset_arena(w, p6, mt);
-    I(s, I_ONE, a) = one;
-    I(s, I_EPISODE, a) = (int)(ep + 1);
+    one_new = one;
+    ep_new = (int)(ep + 1);
     observe(w, o);
   }
   float *stage = lds + kLdsPerLane * 64;  // the TOI / narrow-phase work-list area, free after world_step
@@ -483,8 +515,7 @@ HK_DEV void step_lane(const DevState &s, const KCfg &cfg, const StepIO &io, int6
     observe_two(w, o);
     store_row<18>(io.obs2, a, o, stage, lane);
   }
-  store_arena_changed(w, s, a, m.f, m.i);
-  I(s, I_STEP, a) = (int)(stepc + 1);
+  store_arena_changed(w, s, a, m.f, m.pw, one_new, ep_new, (int)(stepc + 1));
   HK_TIC(T, 12);  // diagnostics: outputs and state store
   out.done_edge = done_edge;
   out.win1 = done_edge && winner == 1;
@@ -548,11 +579,14 @@ HK_DEV void get_state_lane(const DevState &s, int64_t a, float *st, int32_t *aux
     }
   }
   if (aux) {
-    aux[a * 5 + 0] = I(s, I_HAS1, a);
-    aux[a * 5 + 1] = I(s, I_HAS2, a);
-    aux[a * 5 + 2] = I(s, I_TIME, a);
-    aux[a * 5 + 3] = I(s, I_DONE, a);
-    aux[a * 5 + 4] = I(s, I_WINNER, a);
+    uint32_t pw[NPW];
+    int32_t iw[NIF];
+    load_ints(s, a, pw, iw);
+    aux[a * 5 + 0] = iw[I_HAS1];
+    aux[a * 5 + 1] = iw[I_HAS2];
+    aux[a * 5 + 2] = iw[I_TIME];
+    aux[a * 5 + 3] = iw[I_DONE];
+    aux[a * 5 + 4] = iw[I_WINNER];
   }
 }
 
@@ -589,11 +623,13 @@ HK_DEV void set_state_lane(const DevState &s, const KCfg &cfg, int64_t a, const 
 }
 
 HK_DEV void init_lane(const DevState &s, const KCfg &cfg, int64_t a) {
-  for (int k = 0; k < NIF; ++k) I(s, k, a) = 0;
+  // all zero: winner 0 is stored as 1 (PW_ENW), one_starts 0 -- HockeyEnv.__init__ sets one_starts = True and resets
+  // with one_starting=True (hockey_env.py:117,155); hk_create's first reset toggles this 0 -> 1
+  int32_t iw[NIF] = {};
+  uint32_t pw[NPW];
+  pack_ints(iw, pw);
+  for (int k = 0; k < NPW; ++k) PW(s, k, a) = pw[k];
   for (int k = 0; k < NFF; ++k) F(s, k, a) = 0.0f;
-  // HockeyEnv.__init__ sets one_starts = True and resets with one_starting=True (hockey_env.py:117,155);
-  // hk_create's first reset toggles this 0 -> 1.
-  I(s, I_ONE, a) = 0;
   for (int p = 0; p < 3; ++p) {  // row 2: player 2's weak bot under a per-arena override
     const int64_t ga = cfg.arena_offset + a;
     U4 r = philox(cfg.seed, (uint32_t)ga, (uint32_t)(ga >> 32), 0, RNG_PHASE0 + 0x10 * p);

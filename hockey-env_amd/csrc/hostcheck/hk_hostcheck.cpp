@@ -63,7 +63,7 @@ void *hkh_create(int64_t n, const int *cfg6, uint64_t seed, int64_t arena_offset
   HostCtx *c = new HostCtx();
   c->n = n;
   c->f.assign((size_t)NFF * n, 0.0f);
-  c->i.assign((size_t)NIF * n, 0);
+  c->i.assign((size_t)NPW * n, 0);
   c->man.assign((size_t)NSOLID * NMF * n, 0.0f);
   c->phase.assign((size_t)3 * n, 0.0);
   c->counters.assign(16, 0ull);
@@ -134,7 +134,7 @@ void hkh_observe(void *h, float *obs, float *obs2) {
   for (int64_t a = 0; a < c->n; ++a) observe_lane(c->s, c->cfg, a, obs, obs2);
 }
 
-// raw SoA state (diagnostics): f [NFF][N] floats, i [NIF][N] ints
+// raw SoA state (diagnostics): f [NFF][N] floats, i [NPW][N] packed int words
 void hkh_raw(void *h, float **f, int32_t **i) {
   HostCtx *c = (HostCtx *)h;
   *f = c->f.data();

@@ -132,7 +132,8 @@ int hk_set_policy(void *ctx, int player, int policy);
 
 /* Reset the arenas selected by mask ([N] u8, NULL = all).  params ([N,6] f32) is the placement drawn on
  * the host from the reference's PCG64 stream (explicit seeds); NULL = device Philox placement for the
- * context's mode.  max_t ([N] i32) NULL = mode default (250 NORMAL / 80 training).  one_starts ([N] u8)
+ * context's mode.  max_t ([N] i32) NULL = mode default (250 NORMAL / 80 training); values outside [0, 65535] are
+ * rejected with HK_E_INVALID (checked on the host before any launch; r06 packs max_t into 16 bits).  one_starts ([N] u8)
  * is only read when params == NULL (NORMAL puck side); NULL = toggle the per-arena flag like
  * reset(one_starting=None). */
 int hk_reset(void *ctx, const uint8_t *mask, const float *params, const int32_t *max_t,
@@ -162,7 +163,10 @@ int hk_step_host(void *ctx, const float *actions, const double *opp_inc, int32_t
  * launch advance independently instead of meeting at a per-step kernel boundary. */
 int hk_rollout(void *ctx, int32_t n_steps, const hk_step_io *io, void *stream);
 
-/* Raw state access: state [N,18] f32 (body origins / angles / velocities), aux [N,5] i32.
+/* Raw state access: state [N,18] f32 (body origins / angles / velocities), aux [N,5] i32 = has_puck1, has_puck2,
+ * time, done, winner.  hk_set_state rejects aux rows (of the arenas the mask selects) with has_puck outside
+ * [0, 255], done outside {0, 1} or winner outside {-1, 0, 1} with HK_E_INVALID before anything is launched: the
+ * arena's int words are packed in HBM (r06; the reference's values are has_puck 0..15, done 0/1, winner -1/0/1).
  * hk_set_state applies pybox2d setter semantics in set_state's order (SetTransform, SetLinearVelocity wakes,
  * ...); a NaN position pair / angle / velocity pair / omega leaves that quantity's setter uncalled (the
  * reference's set_state never assigns the puck's angle or angular velocity, hockey_env.py:594-608). */

@@ -583,3 +583,40 @@ def test_benchmarked_trajectories_bit_exact_at_full_size(oracle):
     assert c[N.CNT_EPISODES] > n and c[N.CNT_TOI] > 0
     env.close()
     ov.close()
+
+
+def test_packed_int_words_round_trip_and_range_checks():
+    """r06 packs an arena's 12 int words into 6 (hk_kernels.h PW_*): every value in range round-trips through
+    hk_set_state / hk_get_state, hk_step keeps the oracle's time / has_puck / winner semantics (the lockstep tests), and
+    out-of-range aux / max_t rows of the selected arenas are rejected with HK_E_INVALID before anything runs."""
+    from hockey_amd._native import HockeyNativeError
+    from hockey_amd.vec_env import VecHockeyEnv
+
+    n = 8
+    env = VecHockeyEnv(n, device="cuda:0")
+    env.reset(seeds=list(range(n)))
+    st, aux = env.get_state()
+    want = torch.tensor([[0, 0, 0, 0, 0], [15, 0, 251, 1, 1], [0, 15, 7, 1, -1], [255, 255, 123456789, 0, 0],
+                         [3, 4, 2**31 - 1, 1, 1], [1, 2, 3, 0, -1], [0, 0, 0, 1, 0], [9, 0, 80, 0, 1]],
+                        dtype=torch.int32, device="cuda:0")
+    env.set_state(aux=want)
+    _, got = env.get_state()
+    assert torch.equal(got, want)
+    for bad in ([256, 0, 0, 0, 0], [0, -1, 0, 0, 0], [0, 0, 0, 2, 0], [0, 0, 0, 0, 2], [0, 0, 0, 0, -2]):
+        rows = want.clone()
+        rows[5] = torch.tensor(bad, dtype=torch.int32)
+        with pytest.raises(HockeyNativeError):
+            env.set_state(aux=rows)
+        mask = torch.ones(n, dtype=torch.uint8)
+        mask[5] = 0
+        env.set_state(aux=rows, mask=mask)  # the bad row is not selected: accepted
+    _, got = env.get_state()
+    assert torch.equal(got, want)
+    params = torch.zeros((n, 6), dtype=torch.float32)
+    params[:, 0], params[:, 1], params[:, 2], params[:, 3] = 8.0, 4.0, 3.5, 4.0
+    env.reset_params(params, max_t=torch.full((n,), 65535, dtype=torch.int32))
+    with pytest.raises(HockeyNativeError):
+        env.reset_params(params, max_t=torch.full((n,), 65536, dtype=torch.int32))
+    with pytest.raises(HockeyNativeError):
+        env.reset_params(params, max_t=torch.full((n,), -1, dtype=torch.int32))
+    env.close()
