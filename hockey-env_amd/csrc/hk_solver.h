@@ -535,15 +535,24 @@ HK_DEV void vone_chunk(FSlot &s, bool dynA, uint32_t mA, f2 &vA, float &wA, f2 &
   for (; it < stop && active; it += 4) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      // a static body A is +0 at every solve (mA = 0 clears it to +0 bit for bit; lane_mask: no exec branch)
-      vA = f2{mask_f(vA[0], mA), mask_f(vA[1], mA)};
-      wA = mask_f(wA, mA);
+      // a static body A is +0 at every solve (mA = 0 clears it to +0 bit for bit; lane_mask: no exec branch).
+      // kSA: no running lane has a dynamic body A, and the static-A row neither reads nor writes A's velocity
+      // (nor is it written back for a static body), so the reset is dead there and skipped (r06).
+      if constexpr (!kSA) {
+        vA = f2{mask_f(vA[0], mA), mask_f(vA[1], mA)};
+        wA = mask_f(wA, mA);
+      }
       fslot_solve_velocity_p<kSA, kP>(s, vA, wA, vB, wB);
     }
+    // kSA: every running lane's body-A words are 0; kP == 1: every running lane solves one point, so the second
+    // point's impulses never change in this chunk or a later one of this family (the running set only shrinks and
+    // keeps kP == 1) and are left out of the comparison (r06)
     const uint32_t x[10] = {__float_as_uint(vB[0]), __float_as_uint(vB[1]), __float_as_uint(wB),
-                            dynA ? __float_as_uint(vA[0]) : 0u, dynA ? __float_as_uint(vA[1]) : 0u,
-                            dynA ? __float_as_uint(wA) : 0u, __float_as_uint(s.ni[0]), __float_as_uint(s.ni[1]),
-                            __float_as_uint(s.ti[0]), __float_as_uint(s.ti[1])};
+                            kSA ? 0u : (dynA ? __float_as_uint(vA[0]) : 0u),
+                            kSA ? 0u : (dynA ? __float_as_uint(vA[1]) : 0u),
+                            kSA ? 0u : (dynA ? __float_as_uint(wA) : 0u), __float_as_uint(s.ni[0]),
+                            kP == 1 ? sn[7] : __float_as_uint(s.ni[1]), __float_as_uint(s.ti[0]),
+                            kP == 1 ? sn[9] : __float_as_uint(s.ti[1])};
     uint32_t diff = 0u;
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
