@@ -459,6 +459,11 @@ def main():
     if world > 1:
         init_collectives(dist)  # gloo on the GPU path too: host scalars only, no RCCL bring-up
     if gpu:
+        # HK_BENCH_ONE_DEVICE=<d>: every rank on device d -- a multi-rank rehearsal of the real GPU path (gloo
+        # collectives, barriers, max-over-ranks timing, the line) on a one-GPU box; never set by the driver
+        one = os.environ.get("HK_BENCH_ONE_DEVICE")
+        if one is not None:
+            local = int(one)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         sync = torch.cuda.synchronize
