@@ -1000,11 +1000,19 @@ HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, b
   uint32_t sn[19];
 #pragma unroll
   for (int k = 0; k < 19; ++k) sn[k] = 0u;
-  while (wave_any(active && s3)) {
-    const int stop = chunk_end(it);
-    // one variant, per-lane point counts: a second, one-point variant made the kernel spill (the chunk's invariants
-    // hoisted for both; 16 -> 152 B of scratch per lane, 0 -> 33 spilled VGPRs, make resource-usage)
-    vthree_s3_chunk<0, 0>(s0, s1, s2, s3, s2l, mA0, mY, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+  // the point-count variant is picked once per family entry (the running set only shrinks, so one-point stays
+  // one-point), each in its own loop: picking it per chunk inside one loop made the kernel spill (both variants'
+  // invariants hoisted together; 16 -> 152 B of scratch per lane, make resource-usage)
+  if (!wave_any(active && (fs_vcount(s0) != 1 || (s2l && fs_vcount(s1) != 1)))) {
+    while (wave_any(active && s3)) {
+      const int stop = chunk_end(it);
+      vthree_s3_chunk<1, 1>(s0, s1, s2, s3, s2l, mA0, mY, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+    }
+  } else {
+    while (wave_any(active && s3)) {
+      const int stop = chunk_end(it);
+      vthree_s3_chunk<0, 0>(s0, s1, s2, s3, s2l, mA0, mY, dA0, vA0, wA0, vX, wX, vY, wY, sn, it, stop, first, active);
+    }
   }
   if (entered) {
     if (dA0) set_vel_a(B, a0, V2(vA0), wA0);
