@@ -321,28 +321,22 @@ HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &w
     b.x = vn1 - s.bias[0];
     b.y = vn2 - s.bias[1];
     b = vsub(b, V(s.Kxx * a.x + s.Kxy * a.y, s.Kxy * a.x + s.Kyy * a.y));
-    v2 x = vneg(V(s.Nxx * b.x + s.Nxy * b.y, s.Nxy * b.x + s.Nyy * b.y));
-    int ok = 0;
-    if (x.x >= 0.0f && x.y >= 0.0f) ok = 1;
-    if (!ok) {
-      x.x = -s.nm[0] * b.x;
-      x.y = 0.0f;
-      vn2 = s.Kxy * x.x + b.y;
-      if (x.x >= 0.0f && vn2 >= 0.0f) ok = 1;
-    }
-    if (!ok) {
-      x.x = 0.0f;
-      x.y = -s.nm[1] * b.y;
-      vn1 = s.Kxy * x.y + b.x;
-      if (x.y >= 0.0f && vn1 >= 0.0f) ok = 1;
-    }
-    if (!ok) {
-      x.x = 0.0f;
-      x.y = 0.0f;
-      vn1 = b.x;
-      vn2 = b.y;
-      if (vn1 >= 0.0f && vn2 >= 0.0f) ok = 1;
-    }
+    // Box2D's four cases (both points / point 1 only / point 2 only / none), first one that holds wins.  All four
+    // candidates are computed and the winner picked by selects: the same float operations as the if-cascade, without
+    // its exec-mask juggling -- the cascade's short blocks were issued predicated anyway (r06, -DHK_ASM_MARKS dump).
+    const v2 x1 = vneg(V(s.Nxx * b.x + s.Nxy * b.y, s.Nxy * b.x + s.Nyy * b.y));
+    const float x2x = -s.nm[0] * b.x, vn2c = s.Kxy * x2x + b.y;  // case 2: x = (x2x, 0)
+    const float x3y = -s.nm[1] * b.y, vn1c = s.Kxy * x3y + b.x;  // case 3: x = (0, x3y)
+    const bool ok1 = (x1.x >= 0.0f) & (x1.y >= 0.0f);
+    const bool ok2 = (x2x >= 0.0f) & (vn2c >= 0.0f);
+    const bool ok3 = (x3y >= 0.0f) & (vn1c >= 0.0f);
+    const bool ok4 = (b.x >= 0.0f) & (b.y >= 0.0f);  // case 4: x = (0, 0)
+    v2 x;
+    x.x = ok1 ? x1.x : (ok2 ? x2x : 0.0f);
+    x.y = ok1 ? x1.y : ((!ok2 & ok3) ? x3y : 0.0f);
+    const bool ok = ok1 | ok2 | ok3 | ok4;
+    (void)vn1;
+    (void)vn2;
     if (ok) {
       const v2 d = vsub(x, a);
       const f2 P1 = bc(d.x) * normal, P2 = bc(d.y) * normal;

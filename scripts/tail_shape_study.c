@@ -115,6 +115,9 @@ static double key_w[3][NKEY];
 static int nkeys;
 static double gen_mix[2][2];
 static double slow_tot, slow_fam[5];
+static int wide_n[NKEY];
+static char gen_set[2048]; /* multi-contact shapes that keep a chunk in the general family (chunks from it 8) */
+static double gen_by_chunk[8]; /* lanes with >= 4 contacts live at iteration 152, by shape */
 static int key_id(const char *k) {
   for (int i = 0; i < nkeys; ++i)
     if (!strcmp(keys[i], k)) return i;
@@ -193,8 +196,28 @@ int main(int argc, char **argv) {
             cf = all_s2 ? 2 : all_alias ? 2 : 1;
             cost = all_s2 && uniform ? 140 : all_alias ? 180 : 225;
           } else {
-            const int s3 = uniform && !strcmp(k, "[s0p1][10p1][s1p1]") && nmulti > 0;
+            /* S3 family (r06g+): some S3 lane, every other running multi-contact lane S3 or S2 ([01p*][s0p*]) */
+            int any_s3 = 0, all_ok = 1;
+            for (int l = 0; l < 64; ++l) {
+              char key[64];
+              int live;
+              shape_key(&g_rec[w0 + l], t, key, &live);
+              if (live < 2) continue;
+              const int is_s3 = live == 3 && !strcmp(key, "[s0p1][10p1][s1p1]");
+              const int is_s2 = live == 2 && !strncmp(key, "[01p", 4) && !strncmp(key + 6, "[s0p", 4);
+              any_s3 |= is_s3;
+              if (!is_s3 && !is_s2) {
+                all_ok = 0;
+                if (c >= 1 && strlen(gen_set) + strlen(key) + 2 < sizeof gen_set && !strstr(gen_set, key)) {
+                  strcat(gen_set, key);
+                  strcat(gen_set, " ");
+                }
+              }
+            }
+            const int s3 = any_s3 && all_ok;
+            (void)k;
             cf = s3 ? 3 : 4; cost = s3 ? 190 : 109.0 * maxlive;
+            if (!s3) gen_by_chunk[c] += len;
           }
           wf[cf] += cost * len;
           if ((cf == 1 || cf == 4) && c >= 3) { /* generic two-contact or general chunk: the distinct multi-contact shapes running */
@@ -237,6 +260,12 @@ int main(int argc, char **argv) {
         }
       }
     }
+    for (int a = 0; a < n; ++a) { /* lanes still running at the last chunk with >= 4 live contacts: their shapes */
+      char key[64];
+      int live;
+      shape_key(&g_rec[a], 152, key, &live);
+      if (live >= 4) key_w[2][key_id(key)] += 0, wide_n[key_id(key) % NKEY] += 1;
+    }
     slow_tot += best;
     printf("step %d slowest wave %.0f slots (one %.0f two-generic %.0f S2 %.0f S3 %.0f general %.0f): generic-two shapes %s\n",
            st, best, best_fam[0], best_fam[1], best_fam[2], best_fam[3], best_fam[4], best_sig);
@@ -264,6 +293,12 @@ int main(int argc, char **argv) {
   printf("general-family tail iterations per 1000 waves by rider kinds: alone %.1f, +1-contact %.1f, +2-contact "
          "%.1f, +both %.1f\n", 1000 * gen_mix[0][0] / waves, 1000 * gen_mix[1][0] / waves, 1000 * gen_mix[0][1] / waves,
          1000 * gen_mix[1][1] / waves);
+  printf("general-family chunk iterations per 1000 waves by chunk start:");
+  for (int c = 0; c < 8; ++c) printf(" %d:%.1f", starts[c], 1000 * gen_by_chunk[c] / waves);
+  printf("\nshapes that keep a chunk (from iteration 8) in the general family: %s\n", gen_set);
+  printf("lanes with >= 4 contacts still iterating at iteration 152, by shape:\n");
+  for (int i = 0; i < nkeys; ++i)
+    if (wide_n[i]) printf("  %-48s %6d\n", keys[i], wide_n[i]);
   printf("TOI solves by shape (contacts, then per contact points + 2 if body A dynamic): count, mean iterations, "
          ">= 100 iterations\n");
   for (int k = 0; k < 10000; ++k)

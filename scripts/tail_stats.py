@@ -122,3 +122,11 @@ for c in (0, 1, 2, 3, 4):
     if m.any():
         print(f"  class {c}: {m.sum():3d} steps  total {wave_cyc[np.arange(steps), sw][m].mean():9.0f}  " +
               " ".join(f"{PH[k].split('+')[0]} {slow[m, k].mean():7.0f}" for k in (1, 3, 4, 5, 7, 11)))
+# the velocity-family split of those slowest waves (d[21..23]: general + S3 / two-contact / one-contact loop cycles,
+# island and TOI solves together; r06: written by the timers build since the debug-slot fix in hk_kernels.hip)
+sfam = np.stack([D[t, sw[t] * 64:(sw[t] + 1) * 64, 21:24].max(0) for t in range(steps)])  # max over the wave's lanes
+for c in (0, 1, 2, 3, 4):
+    m = ncl_sw[np.arange(steps), sw] == c
+    if m.any():
+        g, t2, o = sfam[m].mean(0)
+        print(f"  class {c}: velocity families  general+S3 {g:9.0f}  two {t2:9.0f}  one {o:9.0f}")
