@@ -762,6 +762,7 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
   const int all = (1 << nisl) - 1;
   S.load_geo(nc, w);
   for (int it = 0; it < kPosIters && (solved & all) != all; ++it) {
+    HK_MARK(pos_begin);
     float ms0 = 0.0f, ms1 = 0.0f, ms2 = 0.0f;
     S.each(nc, [&](FSlot &s, int i) {
       const int isl = fs_isl(s);
@@ -778,6 +779,7 @@ HK_DEV bool solve_islands(Arena &w, SL &S, float dt, PhaseT &T) {
     if (ms0 >= -3.0f * kLinearSlop) solved |= 1;
     if (ms1 >= -3.0f * kLinearSlop) solved |= 2;
     if (ms2 >= -3.0f * kLinearSlop) solved |= 4;
+    HK_MARK(pos_end);
   }
 #pragma unroll
   for (int b = 0; b < 3; ++b)

@@ -352,6 +352,7 @@ HK_DEV void fslot_solve_velocity_p(FSlot &s, f2 &vA, float &wA, f2 &vB, float &w
   }
 }
 
+template <int kP = 0>
 HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
   const int bA = fs_bA(s), bB = fs_bB(s);
   v2 vA, vB;
@@ -359,7 +360,7 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
   get_vel_a(B, bA, vA, wA);
   get_vel_b(B, bB, vB, wB);
   f2 pA = F2(vA), pB = F2(vB);
-  fslot_solve_velocity_p(s, pA, wA, pB, wB);
+  fslot_solve_velocity_p<false, kP>(s, pA, wA, pB, wB);
   set_vel_a(B, bA, V2(pA), wA);
   set_vel_b(B, bB, V2(pB), wB);
 }
@@ -1028,7 +1029,9 @@ HK_DEV void vthree_s3_family(FSlot &s0, FSlot &s1, FSlot &s2, Dyn &B, bool s3, b
 // on its own: an island whose state is periodic retires on its own (its slots leave `live` and are no
 // longer solved; its state at iteration 179 is the current one), while the lane's other islands keep
 // iterating.  With `leave`, it returns after a chunk once no running lane has more than two live contacts.
-template <typename SL>
+// kP == 1: every live contact of every running lane has one point (the caller checks at entry; the running set and
+// the live contacts only shrink), so the rows skip the block solver and the per-slot point-count branch (r06).
+template <typename SL, int kP = 0>
 HK_DEV void vgen_family(SL &S, Dyn &B, int nc, uint32_t &live, const int (&isl_of)[3], int &it, bool &active,
                         int first, bool leave) {
   uint32_t sb[9];
@@ -1050,7 +1053,7 @@ HK_DEV void vgen_family(SL &S, Dyn &B, int nc, uint32_t &live, const int (&isl_o
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         S.each(nc, [&](FSlot &s, int i) {
-          if ((live >> i) & 1u) fslot_solve_velocity(s, B);
+          if ((live >> i) & 1u) fslot_solve_velocity<kP>(s, B);
         });
       uint32_t d0 = 0u, d1 = 0u, d2 = 0u;  // per-island snapshot differences
 #pragma unroll
@@ -1166,7 +1169,10 @@ HK_DEV int velocity_iterations(SL &S, Dyn &B, int nc, const int (&isl_of)[3], Ph
           HK_FAM_ADD(T, 0);
         }
       } else if (wave_any(active && nl > 2)) {
-        vgen_family(S, B, nc, live, isl_of, it, active, first, true);
+        bool p1 = true;  // every live contact one-point
+        S.each(nc, [&](FSlot &s, int i) { p1 = p1 && (((live >> i) & 1u) == 0u || fs_vcount(s) == 1); });
+        if (!wave_any(active && !p1)) vgen_family<SL, 1>(S, B, nc, live, isl_of, it, active, first, true);
+        else vgen_family<SL, 0>(S, B, nc, live, isl_of, it, active, first, true);
         HK_FAM_ADD(T, 0);
       } else {
         const bool fam2 = wave_any(active && nl > 1);
