@@ -147,13 +147,14 @@ HK_DEV rot rot_set(float x) {
   float sn = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r + r;
   float cs = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z -
              0.5f * z + 1.0f;
+  // quadrant j & 3: (s, c) = (sn, cs), (cs, -sn), (-sn, -cs), (-cs, sn) -- by two selects and sign flips (exact
+  // negations) instead of a switch, which compiled to a branch tree with exec-mask juggling (r06, -DHK_ASM_MARKS)
+  const uint32_t k = (uint32_t)j & 3u;
+  const bool odd = (k & 1u) != 0u;
+  const float a = odd ? cs : sn, b = odd ? sn : cs;
   rot q;
-  switch (j & 3) {
-    case 0: q.s = sn; q.c = cs; break;
-    case 1: q.s = cs; q.c = -sn; break;
-    case 2: q.s = -sn; q.c = -cs; break;
-    default: q.s = -cs; q.c = sn; break;
-  }
+  q.s = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, a) ^ ((k & 2u) << 30));
+  q.c = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, b) ^ (((k + 1u) & 2u) << 30));
   return q;
 }
 HK_DEV v2 mul_rv(rot q, v2 v) { return V(q.c * v.x - q.s * v.y, q.s * v.x + q.c * v.y); }

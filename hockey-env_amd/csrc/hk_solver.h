@@ -369,6 +369,7 @@ HK_DEV void fslot_solve_velocity(FSlot &s, Dyn &B) {
 // SolveTOIPositionConstraints' mass gating is the identity (see solve_toi), so one routine serves both.
 // The 2-vector arithmetic is packed (f2): the same float operations in the same order as the scalar form.
 HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float minSep, const ManGeo &m) {
+  HK_MARK(posrow_begin);
   Dyn &B = w.d;
   const float mA = s.mA, mB = s.mB, iA = s.iA, iB = s.iB;
   const int bA = fs_bA(s), bB = fs_bB(s), pcount = fs_pcount(s);
@@ -425,6 +426,7 @@ HK_DEV float fslot_solve_position(const FSlot &s, Arena &w, float baum, float mi
   }
   if (bA < 3) set_pos_a(B, bA, V2(cA), aA);
   set_pos_b(B, bB, V2(cB), aB);
+  HK_MARK(posrow_end);
   return minSep;
 }
 
