@@ -543,35 +543,26 @@ HK_DEV void sep_init(SepFn<PA, PB> &f, const SimplexCache &cache, const PA &pA, 
     if (s < 0.0f) f.axis = vneg(f.axis);
   }
 }
+// The three separation-function types evaluate the same shape of expression with the roles of A / B, the local
+// point and the axis rotation swapped; here the roles are picked by selects and one expression is evaluated, with
+// each type's float operations in its own order.  The cooperative TOI drain runs different pairs (so different
+// types) on the lanes of a wave, and the if-chain ran all three bodies behind exec masks (r06).
 template <typename PA, typename PB>
 HK_DEV float sep_find_min(const SepFn<PA, PB> &f, int &iA, int &iB, float t) {
   HK_EV(EV_SEP_MIN, 1);
   xform xA, xB;
   sweep_xf_of<PA>(f.sA, xA, t);
   sweep_xf_of<PB>(f.sB, xB, t);
-  if (f.type == SF_POINTS) {
-    v2 axA = mulT_rv(xA.q, f.axis), axB = mulT_rv(xB.q, vneg(f.axis));
-    iA = proxy_support(f.pA, axA);
-    iB = proxy_support(f.pB, axB);
-    v2 a = mul_xv(xA, pv(f.pA, iA)), b = mul_xv(xB, pv(f.pB, iB));
-    return dot(vsub(b, a), f.axis);
-  } else if (f.type == SF_FACEA) {
-    v2 normal = mul_rv(xA.q, f.axis);
-    v2 a = mul_xv(xA, f.lp);
-    v2 axB = mulT_rv(xB.q, vneg(normal));
-    iA = -1;
-    iB = proxy_support(f.pB, axB);
-    v2 b = mul_xv(xB, pv(f.pB, iB));
-    return dot(vsub(b, a), normal);
-  } else {
-    v2 normal = mul_rv(xB.q, f.axis);
-    v2 b = mul_xv(xB, f.lp);
-    v2 axA = mulT_rv(xA.q, vneg(normal));
-    iB = -1;
-    iA = proxy_support(f.pA, axA);
-    v2 a = mul_xv(xA, pv(f.pA, iA));
-    return dot(vsub(a, b), normal);
-  }
+  const bool pts = f.type == SF_POINTS, fa = f.type == SF_FACEA, fb = f.type == SF_FACEB;
+  const rot q = fa ? xA.q : xB.q;
+  const v2 nr = mul_rv(q, f.axis);
+  const v2 n = pts ? f.axis : nr;  // points: the axis; face A / B: the axis rotated by A / B
+  const v2 axA = mulT_rv(xA.q, pts ? f.axis : vneg(n)), axB = mulT_rv(xB.q, vneg(n));
+  const int sA = proxy_support(f.pA, axA), sB = proxy_support(f.pB, axB);
+  iA = fa ? -1 : sA;
+  iB = fb ? -1 : sB;
+  const v2 a = mul_xv(xA, fa ? f.lp : pv(f.pA, sA)), b = mul_xv(xB, fb ? f.lp : pv(f.pB, sB));
+  return dot(fb ? vsub(a, b) : vsub(b, a), n);
 }
 template <typename PA, typename PB>
 HK_DEV float sep_eval(const SepFn<PA, PB> &f, int iA, int iB, float t) {
@@ -579,20 +570,12 @@ HK_DEV float sep_eval(const SepFn<PA, PB> &f, int iA, int iB, float t) {
   xform xA, xB;
   sweep_xf_of<PA>(f.sA, xA, t);
   sweep_xf_of<PB>(f.sB, xB, t);
-  if (f.type == SF_POINTS) {
-    v2 a = mul_xv(xA, pv(f.pA, iA)), b = mul_xv(xB, pv(f.pB, iB));
-    return dot(vsub(b, a), f.axis);
-  } else if (f.type == SF_FACEA) {
-    v2 normal = mul_rv(xA.q, f.axis);
-    v2 a = mul_xv(xA, f.lp);
-    v2 b = mul_xv(xB, pv(f.pB, iB));
-    return dot(vsub(b, a), normal);
-  } else {
-    v2 normal = mul_rv(xB.q, f.axis);
-    v2 b = mul_xv(xB, f.lp);
-    v2 a = mul_xv(xA, pv(f.pA, iA));
-    return dot(vsub(a, b), normal);
-  }
+  const bool pts = f.type == SF_POINTS, fa = f.type == SF_FACEA, fb = f.type == SF_FACEB;
+  const rot q = fa ? xA.q : xB.q;
+  const v2 nr = mul_rv(q, f.axis);
+  const v2 n = pts ? f.axis : nr;
+  const v2 a = mul_xv(xA, fa ? f.lp : pv(f.pA, iA)), b = mul_xv(xB, fb ? f.lp : pv(f.pB, iB));
+  return dot(fb ? vsub(a, b) : vsub(b, a), n);
 }
 
 enum { TOI_UNKNOWN = 0, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
